@@ -1,0 +1,302 @@
+// torch bindings for the scaling_amd HIP kernels (module scaling_amd._C).
+// All tensor/dtype/shape validation lives here; kernels see raw pointers and the current HIP stream.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <cmath>
+#include "kernels/launch.h"
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+int dt(const at::Tensor& t) {
+    switch (t.scalar_type()) {
+        case at::kFloat: return DT_F32;
+        case at::kBFloat16: return DT_BF16;
+        case at::kHalf: return DT_F16;
+        default: TORCH_CHECK(false, "scaling_amd: unsupported dtype ", t.scalar_type());
+    }
+    return -1;
+}
+
+void check_cuda(const at::Tensor& t, const char* name) {
+    TORCH_CHECK(t.is_cuda(), "scaling_amd: ", name, " must be a GPU tensor");
+    TORCH_CHECK(t.is_contiguous(), "scaling_amd: ", name, " must be contiguous");
+}
+
+// ------------------------------------------------------------------ norms
+std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                 double eps, bool layer) {
+    check_cuda(x, "x");
+    check_cuda(w, "weight");
+    const int64_t H = x.size(-1);
+    TORCH_CHECK(H % 8 == 0, "norm: hidden size must be a multiple of 8");
+    TORCH_CHECK(w.numel() == H && w.scalar_type() == x.scalar_type(), "norm: weight shape/dtype mismatch");
+    const int64_t rows = x.numel() / H;
+    const at::DeviceGuard g(x.device());
+    auto y = at::empty_like(x);
+    auto opts = x.options().dtype(at::kFloat);
+    auto rstd = at::empty({rows}, opts);
+    auto mean = layer ? at::empty({rows}, opts) : at::empty({0}, opts);
+    const void* bp = nullptr;
+    if (layer) {
+        TORCH_CHECK(b.has_value(), "layernorm needs a bias");
+        check_cuda(*b, "bias");
+        bp = b->data_ptr();
+    }
+    sa_launch::norm_fwd(dt(x), layer, x.data_ptr(), w.data_ptr(), bp, y.data_ptr(),
+                        layer ? mean.data_ptr<float>() : nullptr, rstd.data_ptr<float>(), rows, (int)H, (float)eps,
+                        cur_stream());
+    return {y, mean, rstd};
+}
+
+std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
+                                 const at::Tensor& mean, const at::Tensor& rstd, bool layer) {
+    check_cuda(dy, "dy");
+    check_cuda(x, "x");
+    const int64_t H = x.size(-1);
+    const int64_t rows = x.numel() / H;
+    const at::DeviceGuard g(x.device());
+    auto dx = at::empty_like(x);
+    auto dw = at::empty_like(w);
+    auto db = layer ? at::empty_like(w) : at::empty({0}, w.options());
+    const int nw = sa_launch::norm_bwd_waves(rows);
+    auto part = at::empty({(layer ? 2 : 1) * (int64_t)nw * H}, x.options().dtype(at::kFloat));
+    sa_launch::norm_bwd(dt(x), layer, dy.data_ptr(), x.data_ptr(), w.data_ptr(),
+                        layer ? mean.data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
+                        dw.data_ptr(), layer ? db.data_ptr() : nullptr, part.data_ptr<float>(), rows, (int)H,
+                        cur_stream());
+    return {dx, dw, db};
+}
+
+
+// ------------------------------------------------------------------ swiglu
+// z: [..., 2F] (a | b halves) or separate a/b with equal row stride
+at::Tensor swiglu_fwd(const at::Tensor& a, const at::Tensor& b) {
+    TORCH_CHECK(a.is_cuda() && b.is_cuda(), "swiglu: GPU tensors required");
+    TORCH_CHECK(a.sizes() == b.sizes() && a.stride(-1) == 1 && b.stride(-1) == 1 && a.stride(-2) == b.stride(-2),
+                "swiglu: a/b must share shape and row stride");
+    const int64_t F = a.size(-1);
+    TORCH_CHECK(F % 8 == 0, "swiglu: feature size must be a multiple of 8");
+    const int64_t rows = a.numel() / F;
+    const at::DeviceGuard g(a.device());
+    auto out = at::empty(a.sizes(), a.options());
+    sa_launch::swiglu_fwd(dt(a), a.data_ptr(), b.data_ptr(), a.stride(-2), out.data_ptr(), rows, (int)F, cur_stream());
+    return out;
+}
+std::vector<at::Tensor> swiglu_bwd(const at::Tensor& dy, const at::Tensor& a, const at::Tensor& b, bool fused_out) {
+    const int64_t F = a.size(-1);
+    const int64_t rows = a.numel() / F;
+    const at::DeviceGuard g(a.device());
+    auto dyc = dy.contiguous();
+    if (fused_out) {
+        auto sizes = a.sizes().vec();
+        sizes.back() = 2 * F;
+        auto dz = at::empty(sizes, a.options());
+        sa_launch::swiglu_bwd(dt(a), dyc.data_ptr(), a.data_ptr(), b.data_ptr(), a.stride(-2), dz.data_ptr(),
+                              (char*)dz.data_ptr() + F * dz.element_size(), 2 * F, rows, (int)F, cur_stream());
+        return {dz};
+    }
+    auto da = at::empty(a.sizes(), a.options());
+    auto db = at::empty(a.sizes(), a.options());
+    sa_launch::swiglu_bwd(dt(a), dyc.data_ptr(), a.data_ptr(), b.data_ptr(), a.stride(-2), da.data_ptr(), db.data_ptr(),
+                          F, rows, (int)F, cur_stream());
+    return {da, db};
+}
+
+// ------------------------------------------------------------------ rope
+// x: [T, nh, hd] (any token/head stride, unit element stride) -> contiguous [T, nh, hd]
+at::Tensor rope(const at::Tensor& x, const at::Tensor& cosb, const at::Tensor& sinb, const c10::optional<at::Tensor>& pos,
+                int64_t rot_dim, int64_t seq_len, bool interleaved, bool inverse) {
+    TORCH_CHECK(x.is_cuda() && x.dim() == 3 && x.stride(2) == 1, "rope: x must be [T, nh, hd] with unit last stride");
+    TORCH_CHECK(cosb.scalar_type() == at::kFloat && cosb.is_contiguous() && sinb.is_contiguous(), "rope: fp32 tables");
+    const int64_t T = x.size(0), nh = x.size(1), hd = x.size(2);
+    TORCH_CHECK(rot_dim % 2 == 0 && rot_dim <= hd && cosb.size(-1) == rot_dim / 2, "rope: bad rotary dims");
+    const at::DeviceGuard g(x.device());
+    auto out = at::empty({T, nh, hd}, x.options());
+    const int64_t* pp = nullptr;
+    at::Tensor pc;
+    if (pos.has_value()) {
+        pc = pos->to(at::kLong).contiguous();
+        TORCH_CHECK(pc.numel() == T, "rope: position ids must have one entry per token");
+        pp = pc.data_ptr<int64_t>();
+    }
+    sa_launch::rope(dt(x), interleaved, x.data_ptr(), x.stride(0), x.stride(1), out.data_ptr(), cosb.data_ptr<float>(),
+                    sinb.data_ptr<float>(), pp, T, (int)nh, (int)hd, (int)rot_dim, (int)seq_len, inverse ? -1.f : 1.f,
+                    cur_stream());
+    return out;
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<at::Tensor> xent_stats(const at::Tensor& logits, const at::Tensor& target, int64_t v0) {
+    check_cuda(logits, "logits");
+    const int64_t V = logits.size(-1), rows = logits.numel() / V;
+    TORCH_CHECK(V % 8 == 0 || true, "");
+    const at::DeviceGuard g(logits.device());
+    auto t = target.to(at::kLong).contiguous();
+    auto fo = logits.options().dtype(at::kFloat);
+    auto m = at::empty({rows}, fo), s = at::empty({rows}, fo), tl = at::empty({rows}, fo);
+    auto am = at::empty({rows}, logits.options().dtype(at::kLong));
+    sa_launch::xent_stats(dt(logits), logits.data_ptr(), t.data_ptr<int64_t>(), rows, (int)V, v0, m.data_ptr<float>(),
+                          s.data_ptr<float>(), tl.data_ptr<float>(), am.data_ptr<int64_t>(), cur_stream());
+    return {m, s, tl, am};
+}
+at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& target, const at::Tensor& lse, const at::Tensor& gscale,
+                    int64_t v0, bool inplace) {
+    check_cuda(logits, "logits");
+    const int64_t V = logits.size(-1), rows = logits.numel() / V;
+    const at::DeviceGuard g(logits.device());
+    auto t = target.to(at::kLong).contiguous();
+    auto out = inplace ? logits : at::empty_like(logits);
+    sa_launch::xent_bwd(dt(logits), logits.data_ptr(), t.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                        gscale.data_ptr<float>(), out.data_ptr(), rows, (int)V, v0, cur_stream());
+    return out;
+}
+
+// ------------------------------------------------------------------ embedding
+at::Tensor embed_fwd(const at::Tensor& ids, const at::Tensor& W, int64_t v0) {
+    check_cuda(W, "weight");
+    const int64_t H = W.size(1);
+    TORCH_CHECK(H % 8 == 0, "embedding: hidden size must be a multiple of 8");
+    const at::DeviceGuard g(W.device());
+    auto idc = ids.to(at::kLong).contiguous();
+    auto sizes = idc.sizes().vec();
+    sizes.push_back(H);
+    auto out = at::empty(sizes, W.options());
+    sa_launch::embed_fwd(dt(W), idc.data_ptr<int64_t>(), W.data_ptr(), out.data_ptr(), idc.numel(), (int)H, v0,
+                         W.size(0), cur_stream());
+    return out;
+}
+at::Tensor embed_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t num_rows, int64_t v0) {
+    const int64_t H = dy.size(-1);
+    const at::DeviceGuard g(dy.device());
+    auto idc = ids.to(at::kLong).reshape({-1});
+    auto sorted = at::sort(idc, /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    auto sid = std::get<0>(sorted).contiguous();
+    auto order = std::get<1>(sorted).contiguous();
+    auto uc = at::unique_consecutive(sid, /*return_inverse=*/false, /*return_counts=*/true);
+    auto uniq = std::get<0>(uc).contiguous();
+    auto counts = std::get<2>(uc);
+    auto seg = at::zeros({uniq.numel() + 1}, idc.options());
+    seg.narrow(0, 1, uniq.numel()).copy_(at::cumsum(counts, 0));
+    auto dW = at::zeros({num_rows, H}, dy.options());
+    auto dyc = dy.contiguous();
+    sa_launch::embed_bwd(dt(dyc), dyc.data_ptr(), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
+                         uniq.data_ptr<int64_t>(), uniq.numel(), dW.data_ptr(), (int)H, v0, num_rows, cur_stream());
+    return dW;
+}
+
+// ------------------------------------------------------------------ optimizer
+void adamw_(at::Tensor p, const at::Tensor& grad, at::Tensor m, at::Tensor v, c10::optional<at::Tensor> pout, double lr,
+            double b1, double b2, double eps, double wd, int64_t step, double gscale) {
+    TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+                "adamw: fp32 master/state");
+    TORCH_CHECK(p.is_contiguous() && grad.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adamw: contiguous");
+    TORCH_CHECK(p.numel() == grad.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adamw: sizes");
+    const at::DeviceGuard g(p.device());
+    void* po = nullptr;
+    int pdt = DT_F32;
+    if (pout.has_value() && pout->defined()) {
+        TORCH_CHECK(pout->numel() == p.numel() && pout->is_contiguous(), "adamw: param out");
+        po = pout->data_ptr();
+        pdt = dt(*pout);
+    }
+    const double bc1 = 1.0 - std::pow(b1, (double)step);
+    const double bc2 = 1.0 - std::pow(b2, (double)step);
+    sa_launch::adamw(dt(grad), pdt, p.data_ptr<float>(), grad.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(), po,
+                     p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1,
+                     (float)std::sqrt(bc2), (float)gscale, cur_stream());
+}
+// accumulates (sum of squares, count of non-finite) of x*scale into out[0], out[1] (fp32, on device)
+void sumsq_(const at::Tensor& x, at::Tensor out, double scale, bool accumulate) {
+    TORCH_CHECK(x.is_contiguous() && out.scalar_type() == at::kFloat && out.numel() >= 2, "sumsq: bad args");
+    const at::DeviceGuard g(x.device());
+    const int nb = sa_launch::sumsq_blocks(x.numel());
+    auto part = at::empty({2 * nb}, out.options());
+    float* o = out.data_ptr<float>();
+    sa_launch::sumsq(dt(x), x.data_ptr(), x.numel(), (float)scale, part.data_ptr<float>(), part.data_ptr<float>() + nb,
+                     o, o + 1, accumulate ? 1 : 0, cur_stream());
+}
+void cast_scale_(const at::Tensor& x, at::Tensor y, double scale) {
+    TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "cast_scale: bad args");
+    const at::DeviceGuard g(x.device());
+    sa_launch::cast_scale(dt(x), dt(y), x.data_ptr(), y.data_ptr(), x.numel(), (float)scale, cur_stream());
+}
+
+// ------------------------------------------------------------------ flash attention
+void check_qkv(const at::Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 3 && t.stride(2) == 1, "flash_attn: ", n, " must be [T, heads, D] with unit last stride");
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash_attn: ", n, " must be bfloat16");
+    TORCH_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0, "flash_attn: ", n, " strides must be multiples of 8");
+}
+std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& cu_q,
+                               const at::Tensor& cu_k, int64_t max_q, double scale, bool causal, int64_t window) {
+    check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
+    const int64_t D = q.size(2);
+    TORCH_CHECK(D == 32 || D == 64 || D == 128, "flash_attn: head dim must be 32, 64 or 128");
+    TORCH_CHECK(k.size(2) == D && v.size(2) == D && k.size(1) == v.size(1) && q.size(1) % k.size(1) == 0, "flash_attn: shapes");
+    TORCH_CHECK(cu_q.scalar_type() == at::kInt && cu_k.scalar_type() == at::kInt && cu_q.numel() == cu_k.numel(), "flash_attn: cu_seqlens int32");
+    const at::DeviceGuard g(q.device());
+    const int64_t T = q.size(0), H = q.size(1);
+    auto o = at::empty({T, H, D}, q.options());
+    auto lse = at::empty({H, T}, q.options().dtype(at::kFloat));
+    FwdArgs a{};
+    a.q = (const uint16_t*)q.data_ptr(); a.k = (const uint16_t*)k.data_ptr(); a.v = (const uint16_t*)v.data_ptr();
+    a.o = (uint16_t*)o.data_ptr(); a.lse = lse.data_ptr<float>();
+    a.q_tok = q.stride(0); a.q_head = q.stride(1); a.k_tok = k.stride(0); a.k_head = k.stride(1);
+    a.v_tok = v.stride(0); a.v_head = v.stride(1); a.o_tok = o.stride(0); a.o_head = o.stride(1); a.lse_stride = T;
+    a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
+    a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)k.size(1); a.causal = causal ? 1 : 0; a.window = (int)window;
+    a.scale_log2 = (float)(scale * 1.4426950408889634);
+    if (T > 0 && a.nseg > 0) sa_launch::fa_fwd(a, (int)D, (int)max_q, cur_stream());
+    return {o, lse};
+}
+std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                               const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_q, const at::Tensor& cu_k,
+                               int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window) {
+    check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(o, "o");
+    auto dO = dout.contiguous();
+    check_qkv(dO, "dout");
+    const int64_t D = q.size(2), T = q.size(0), H = q.size(1), Tk = k.size(0), Hk = k.size(1);
+    const at::DeviceGuard g(q.device());
+    auto dq = at::empty({T, H, D}, q.options());
+    auto dk = at::empty({Tk, Hk, D}, k.options());
+    auto dv = at::empty({Tk, Hk, D}, v.options());
+    auto delta = at::empty({H, T}, q.options().dtype(at::kFloat));
+    BwdArgs a{};
+    a.q = (const uint16_t*)q.data_ptr(); a.k = (const uint16_t*)k.data_ptr(); a.v = (const uint16_t*)v.data_ptr();
+    a.dO = (const uint16_t*)dO.data_ptr(); a.lse = lse.data_ptr<float>(); a.delta = delta.data_ptr<float>();
+    a.dq = (uint16_t*)dq.data_ptr(); a.dk = (uint16_t*)dk.data_ptr(); a.dv = (uint16_t*)dv.data_ptr();
+    a.q_tok = q.stride(0); a.q_head = q.stride(1); a.k_tok = k.stride(0); a.k_head = k.stride(1);
+    a.v_tok = v.stride(0); a.v_head = v.stride(1); a.do_tok = dO.stride(0); a.do_head = dO.stride(1);
+    a.dq_tok = dq.stride(0); a.dq_head = dq.stride(1); a.dk_tok = dk.stride(0); a.dk_head = dk.stride(1);
+    a.dv_tok = dv.stride(0); a.dv_head = dv.stride(1); a.lse_stride = T;
+    a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
+    a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)Hk; a.causal = causal ? 1 : 0; a.window = (int)window;
+    a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
+    if (T > 0 && a.nseg > 0)
+        sa_launch::fa_bwd(a, (const uint16_t*)o.data_ptr(), o.stride(0), o.stride(1), T, (int)D, (int)max_q, (int)max_k,
+                          cur_stream());
+    return {dq, dk, dv};
+}
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "scaling_amd CDNA4 (gfx950) HIP kernels";
+    m.def("norm_fwd", &norm_fwd, "RMSNorm/LayerNorm forward");
+    m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward");
+    m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
+    m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
+    m.def("rope", &rope, "rotary embedding (fwd / inverse)");
+    m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
+    m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
+    m.def("embed_fwd", &embed_fwd, "vocab-parallel embedding forward");
+    m.def("embed_bwd", &embed_bwd, "deterministic embedding backward");
+    m.def("adamw_", &adamw_, "fused AdamW on flat fp32 buffers");
+    m.def("sumsq_", &sumsq_, "sum of squares + non-finite count");
+    m.def("cast_scale_", &cast_scale_, "y = cast(x * scale)");
+    m.def("fa_fwd", &fa_fwd, "flash attention forward");
+    m.def("fa_bwd", &fa_bwd, "flash attention backward");
+}

@@ -1,0 +1,97 @@
+// Flash-attention building blocks for gfx950 (MFMA 32x32x16 bf16, wave64).
+//
+// Conventions (cdna_hip_programming.md §3, "An accumulator tile as the next MFMA's operand"):
+//  * mfma_f32_32x32x16_bf16 operands: lane l (r = l&31, h = l>>5) holds A[r][8h+j], B[8h+j][r];
+//    C/D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*h.
+//  * "swapped" products keep the query (fwd, dQ) or the key (dK/dV) on the lane, so every softmax
+//    row statistic is lane-local and an accumulator feeds the next MFMA as its B operand with no
+//    lane movement (k order inside a step permuted: element j <-> row 16s + 8(j>>2) + 4h + (j&3)).
+//  * The transposed operand of that next product is read with ds_read_b64_tr_b16.
+//  * One LDS image per tile serves both row reads (ds_read_b128) and transposed reads: the
+//    16-B chunk swizzle of §5.5 T10 "One image for row reads AND transposed reads" (b), extended
+//    to 64/32-wide heads (see SWZ below) — conflict-free for both read kinds.
+#pragma once
+#include "common.h"
+
+namespace sa {
+namespace fa {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <int D>
+__device__ __forceinline__ int swz(int r, int c) {
+    if constexpr (D == 128) return c ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    else if constexpr (D == 64) return c ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+    else return c ^ ((r >> 2) & 3);  // D == 32
+}
+
+// byte offset of element (r, d) in a [rows][D] bf16 LDS image
+template <int D>
+__device__ __forceinline__ int lds_off(int r, int d) {
+    return r * D * 2 + 16 * swz<D>(r, d >> 3) + ((d & 7) << 1);
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// row read: 8 bf16 of row r starting at column d (d multiple of 8)
+template <int D>
+__device__ __forceinline__ bf16x8 ld_row(const char* lds, int r, int d) {
+    return *reinterpret_cast<const bf16x8*>(lds + lds_off<D>(r, d));
+}
+
+// transposed A-operand fragment of X^T where X is a [rows][D] tile: lane receives
+// X[kb + 4h + q][col] (q=0..3) and X[kb + 8 + 4h + q][col] for col = c0 + (l&31).
+template <int D>
+__device__ __forceinline__ bf16x8 ld_tr(const char* lds, int kb, int c0) {
+    const int l = threadIdx.x & 63;
+    const int h = l >> 5, g = (l >> 4) & 1, i = l & 15;
+    const int row = kb + 4 * h + (i >> 2);
+    const int col = c0 + 16 * g + 4 * (i & 3);
+    s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lds_off<D>(row, col)));
+    s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lds_off<D>(row + 8, col)));
+    s16x4 c = {a[0], a[1], a[2], a[3]};
+    typedef short s16x8v __attribute__((ext_vector_type(8)));
+    s16x8v r = {c[0], c[1], c[2], c[3], b[0], b[1], b[2], b[3]};
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+// pack accumulator registers 8s..8s+7 into a bf16 B-operand fragment
+__device__ __forceinline__ bf16x8 pack_acc(const f32x16& acc, int s) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+    return r;
+}
+
+// global -> register staging of a [64][D] tile (rows beyond `valid` read as zero), 256 threads.
+template <int D>
+struct Stage {
+    static constexpr int NPT = 64 * D / 8 / 256;
+    u16x8 r[NPT];
+    __device__ __forceinline__ void load(const u16* base, int64_t tok_stride, int valid) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int id = threadIdx.x + i * 256;
+            const int row = id / (D / 8), c = id % (D / 8);
+            if (row < valid) r[i] = *reinterpret_cast<const u16x8*>(base + (int64_t)row * tok_stride + c * 8);
+            else r[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+    __device__ __forceinline__ void store(char* lds) {
+#pragma unroll
+        for (int i = 0; i < NPT; ++i) {
+            const int id = threadIdx.x + i * 256;
+            const int row = id / (D / 8), c = id % (D / 8);
+            *reinterpret_cast<u16x8*>(lds + row * D * 2 + 16 * swz<D>(row, c)) = r[i];
+        }
+    }
+};
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+}  // namespace fa
+}  // namespace sa

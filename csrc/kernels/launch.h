@@ -1,0 +1,71 @@
+// Host-side launcher declarations shared between the HIP kernel TUs and the torch bindings.
+// Kernels take raw pointers + a hipStream_t; bindings.cpp owns all tensor/dtype checking.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+enum SaDType { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
+
+namespace sa_launch {
+// norm.hip
+void norm_fwd(int dtype, bool layer, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+              int64_t rows, int H, float eps, hipStream_t st);
+int norm_bwd_waves(int64_t rows);
+void norm_bwd(int dtype, bool layer, const void* dy, const void* x, const void* w, const float* mean,
+              const float* rstd, void* dx, void* dw, void* db, float* part, int64_t rows, int H, hipStream_t st);
+}  // namespace sa_launch
+
+namespace sa_launch {
+// swiglu_rope.hip
+void swiglu_fwd(int dtype, const void* a, const void* b, int64_t lda, void* out, int64_t rows, int F, hipStream_t st);
+void swiglu_bwd(int dtype, const void* dy, const void* a, const void* b, int64_t lda, void* da, void* db, int64_t ldd,
+                int64_t rows, int F, hipStream_t st);
+void rope(int dtype, bool interleaved, const void* x, int64_t tok_stride, int64_t head_stride, void* out,
+          const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd, int seq_len,
+          float sign, hipStream_t st);
+}  // namespace sa_launch
+
+namespace sa_launch {
+// xent_embed_optim.hip
+void xent_stats(int dtype, const void* logits, const int64_t* tgt, int64_t rows, int V, int64_t v0, float* m, float* s,
+                float* t, int64_t* amax, hipStream_t st);
+void xent_bwd(int dtype, const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
+              int64_t rows, int V, int64_t v0, hipStream_t st);
+void embed_fwd(int dtype, const int64_t* ids, const void* W, void* out, int64_t ntok, int H, int64_t v0, int64_t Vp,
+               hipStream_t st);
+void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* seg, const int64_t* seg_id, int64_t nseg,
+               void* dW, int H, int64_t v0, int64_t Vp, hipStream_t st);
+void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, void* pout, int64_t n, float lr,
+           float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale, hipStream_t st);
+int sumsq_blocks(int64_t n);
+void sumsq(int dtype, const void* x, int64_t n, float scale, float* part_sq, float* part_bad, float* out_sq,
+           float* out_bad, int accumulate, hipStream_t st);
+void cast_scale(int sdt, int ddt, const void* x, void* y, int64_t n, float scale, hipStream_t st);
+}  // namespace sa_launch
+
+// flash attention (bf16, head dim 32/64/128)
+struct FwdArgs {
+    const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o; float* lse;
+    int64_t q_tok, q_head, k_tok, k_head, v_tok, v_head, o_tok, o_head, lse_stride;
+    const int* cu_q; const int* cu_k;
+    int nseg, Hq, Hkv, causal, window;
+    float scale_log2;
+};
+namespace sa_launch {
+void fa_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st);
+}
+
+struct BwdArgs {
+    const uint16_t* q; const uint16_t* k; const uint16_t* v; const uint16_t* dO;
+    const float* lse; float* delta;
+    uint16_t* dq; uint16_t* dk; uint16_t* dv;
+    int64_t q_tok, q_head, k_tok, k_head, v_tok, v_head, do_tok, do_head;
+    int64_t dq_tok, dq_head, dk_tok, dk_head, dv_tok, dv_head, lse_stride;
+    const int* cu_q; const int* cu_k;
+    int nseg, Hq, Hkv, causal, window;
+    float scale, scale_log2;
+};
+namespace sa_launch {
+void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
+            hipStream_t st);
+}

@@ -1,0 +1,123 @@
+"""In-tree builder for the scaling_amd native extensions (gfx950 HIP + C++ host code).
+
+No hipify, no torch JIT: every ``csrc/**/*.hip`` is compiled by ``hipcc --offload-arch=gfx950`` and
+``csrc/**/*.cpp`` by hipcc as host C++, then linked against torch's bundled HIP runtime into
+``scaling_amd/_C<EXT_SUFFIX>``.  Objects are cached by content hash under ``build/``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "objs"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+EXT_NAME = "_C"
+
+
+def _torch_paths() -> tuple[list[str], list[str]]:
+    import torch
+
+    tdir = Path(torch.__file__).parent
+    inc = [str(tdir / "include"), str(tdir / "include" / "torch" / "csrc" / "api" / "include"), "/opt/rocm/include"]
+    lib = [str(tdir / "lib")]
+    return inc, lib
+
+
+def _hipcc() -> str:
+    return os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _common_flags(inc: list[str]) -> list[str]:
+    import torch
+
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = [
+        "-O3",
+        "-fPIC",
+        "-std=c++17",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DUSE_ROCM=1",
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DTORCH_EXTENSION_NAME=" + EXT_NAME,
+        "-DTORCH_API_INCLUDE_EXTENSION_H",
+        "-Wno-unused-result",
+        "-Wno-deprecated-declarations",
+        f"-I{CSRC}",
+        f"-I{sysconfig.get_paths()['include']}",
+    ]
+    flags += [f"-I{p}" for p in inc]
+    return flags
+
+
+def _sources() -> list[Path]:
+    return sorted(list(CSRC.rglob("*.hip")) + list(CSRC.rglob("*.cpp")))
+
+
+def _obj_for(src: Path, flags: list[str]) -> Path:
+    h = hashlib.sha1()
+    h.update(src.read_bytes())
+    for hdr in sorted(CSRC.rglob("*.h")):
+        h.update(hdr.read_bytes())
+    h.update(" ".join(flags).encode())
+    return BUILD / f"{src.stem}-{h.hexdigest()[:16]}.o"
+
+
+def _compile(src: Path, flags: list[str]) -> Path:
+    obj = _obj_for(src, flags)
+    if obj.exists():
+        return obj
+    if src.suffix == ".hip":
+        cmd = [_hipcc()] + flags + [f"--offload-arch={ARCH}", "-mcode-object-version=5", "-x", "hip"]
+    else:
+        # host-only TU (bindings, data-pipeline C++): plain g++, no device code generation
+        cmd = [os.environ.get("CXX", "g++")] + flags + ["-fopenmp"]
+    cmd += ["-c", str(src), "-o", str(obj) + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(str(obj) + ".tmp", obj)
+    return obj
+
+
+def ext_path() -> Path:
+    return ROOT / "scaling_amd" / (EXT_NAME + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build(verbose: bool = True, jobs: int | None = None) -> Path:
+    inc, lib = _torch_paths()
+    flags = _common_flags(inc)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    srcs = _sources()
+    jobs = jobs or min(8, os.cpu_count() or 4, len(srcs))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, flags), srcs))
+    out = ext_path()
+    h = hashlib.sha1("".join(str(o) for o in objs).encode()).hexdigest()[:16]
+    stamp = BUILD / f"link-{h}.stamp"
+    if out.exists() and stamp.exists():
+        return out
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out) + ".tmp"] + [str(o) for o in objs]
+    for p in lib:
+        cmd += [f"-L{p}", f"-Wl,-rpath,{p}"]
+    cmd += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lgomp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(str(out) + ".tmp", out)
+    for old in BUILD.glob("link-*.stamp"):
+        old.unlink()
+    stamp.touch()
+    if verbose:
+        print(f"[scaling_amd] built {out.name} from {len(srcs)} sources", file=sys.stderr)
+    return out
+
+
+if __name__ == "__main__":
+    build()

@@ -1,0 +1,13 @@
+from .rng_tracker import CudaRNGStateTracker, RngTrackerState
+from .topology import Topology, TopologyState
+from .topology_config import ActivationCheckpointingType, PipePartitionMethod, TopologyConfig
+
+__all__ = [
+    "ActivationCheckpointingType",
+    "CudaRNGStateTracker",
+    "PipePartitionMethod",
+    "RngTrackerState",
+    "Topology",
+    "TopologyConfig",
+    "TopologyState",
+]

@@ -1,0 +1,40 @@
+"""Loader for the in-tree HIP extension (``scaling_amd._C``).
+
+Policy: a GPU tensor ALWAYS goes through the HIP kernels; if the extension is missing on a GPU box the
+op raises (no silent eager fallback).  CPU tensors (gloo CI, numerics oracles) use the pure-torch
+reference implementations that live next to each op.
+"""
+from __future__ import annotations
+
+from types import ModuleType
+from typing import Optional
+
+import torch
+
+_EXT: Optional[ModuleType] = None
+
+
+def ext() -> ModuleType:
+    global _EXT
+    if _EXT is None:
+        try:
+            from scaling_amd import _C  # type: ignore[attr-defined]
+        except ImportError as e:  # pragma: no cover - depends on build state
+            raise RuntimeError(
+                "scaling_amd HIP extension is not built (python -c 'import __graft_entry__ as g; g.build()' "
+                "or python -m scaling_amd._build)"
+            ) from e
+        _EXT = _C
+    return _EXT
+
+
+def use_native(*tensors: torch.Tensor) -> bool:
+    return any(t is not None and t.is_cuda for t in tensors)
+
+
+def available() -> bool:
+    try:
+        ext()
+        return True
+    except RuntimeError:
+        return False

@@ -1,0 +1,223 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from scaling_amd.ops import attention, embedding, norm, optim, rope, swiglu, xent  # noqa: E402
+from scaling_amd.ops._ext import ext  # noqa: E402
+
+DEV = "cuda"
+
+
+def test_extension_is_native():
+    assert ext().__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H", [256, 4096, 1000 - 1000 % 8])
+def test_rms_norm(dtype, H):
+    torch.manual_seed(0)
+    x = torch.randn(37, 5, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_(True)
+    y = norm.rms_norm(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = norm.rms_norm_reference(xr, wr, 1e-5)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=tol * 20, rtol=tol * 2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layer_norm(dtype):
+    torch.manual_seed(0)
+    H = 768
+    x = torch.randn(64, 3, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_(True)
+    y = norm.layer_norm(x, w, b, 1e-5)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=tol * 20, rtol=tol * 2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=tol * 20, rtol=tol * 2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_swiglu_fused(dtype):
+    torch.manual_seed(0)
+    z = torch.randn(33, 7, 2 * 344, device=DEV, dtype=dtype, requires_grad=True)
+    y = swiglu.swiglu_fused(z)
+    zr = z.detach().float().requires_grad_(True)
+    yr = swiglu.swiglu_reference(zr[..., :344], zr[..., 344:])
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(z.grad.float(), zr.grad, atol=tol * 2, rtol=tol * 2)
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+@pytest.mark.parametrize("rot_frac", [1.0, 0.5])
+def test_rope(interleaved, rot_frac):
+    torch.manual_seed(0)
+    T, nh, hd = 96, 6, 64
+    rd = int(hd * rot_frac)
+    qkv = torch.randn(T, nh, 3 * hd, device=DEV, dtype=torch.bfloat16)
+    x = qkv[:, :, hd : 2 * hd].detach().requires_grad_(True)  # strided view
+    cos, sin = rope.rope_tables(rd, 128, 10000, interleaved, torch.bfloat16, DEV)
+    pos = torch.randint(0, 128, (T,), device=DEV)
+    y = rope.apply_rope(x, cos, sin, pos, rd, 48, interleaved)
+    xr = x.detach().float().requires_grad_(True)
+    yr = rope.rope_reference(xr, cos, sin, pos, rd, 48, interleaved)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2, rtol=3e-2)
+    # no position ids -> position = t % seq_len
+    y2 = rope.apply_rope(x.detach(), cos, sin, None, rd, 48, interleaved)
+    y2r = rope.rope_reference(x.detach().float(), cos, sin, None, rd, 48, interleaved)
+    torch.testing.assert_close(y2.float(), y2r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("V", [1000, 32000])
+def test_cross_entropy(V):
+    torch.manual_seed(0)
+    N = 67
+    logits = (3 * torch.randn(N, V, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    loss, am = xent.vocab_parallel_cross_entropy(logits, tgt)
+    lr = logits.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, tgt, reduction="none")
+    torch.testing.assert_close(loss, ref, atol=1e-4, rtol=1e-4)
+    assert torch.equal(am, lr.argmax(-1))
+    w = torch.rand(N, device=DEV)
+    (loss * w).sum().backward()
+    (ref * w).sum().backward()
+    torch.testing.assert_close(logits.grad.float(), lr.grad, atol=2e-3, rtol=2e-2)
+
+
+def test_embedding():
+    torch.manual_seed(0)
+    Vp, H = 500, 256
+    W = torch.randn(Vp, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, 1000, (4, 33), device=DEV)
+    out = embedding.vocab_embedding(ids, W, 250, 750)
+    Wr = W.detach().float().requires_grad_(True)
+    ref = embedding.vocab_embedding_reference(ids, Wr, 250, 750)
+    torch.testing.assert_close(out.float(), ref)
+    g = torch.randn_like(out)
+    out.backward(g)
+    ref.backward(g.float())
+    torch.testing.assert_close(W.grad.float(), Wr.grad, atol=5e-2, rtol=2e-2)
+    # determinism
+    W.grad = None
+    embedding.vocab_embedding(ids, W, 250, 750).backward(g)
+    g1 = W.grad.clone()
+    W.grad = None
+    embedding.vocab_embedding(ids, W, 250, 750).backward(g)
+    assert torch.equal(g1, W.grad)
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(0)
+    n = 10007
+    p0 = torch.randn(n, device=DEV)
+    ref = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    p, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pout = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    for step in range(1, 6):
+        g = torch.randn(n, device=DEV)
+        ref.grad = g.clone()
+        opt.step()
+        optim.adamw_step_(p, g.to(torch.bfloat16).float(), m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8,
+                          weight_decay=0.1, step=step, param_out=pout) if False else optim.adamw_step_(
+            p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step, param_out=pout)
+    torch.testing.assert_close(p, ref.detach(), atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(pout.float(), ref.detach(), atol=1e-2, rtol=1e-2)
+
+
+def test_sumsq():
+    x = torch.randn(123457, device=DEV, dtype=torch.bfloat16)
+    out = torch.zeros(2, device=DEV)
+    optim.sumsq_nonfinite_(x, out, scale=0.5, accumulate=False)
+    ref = ((x.float() * 0.5) ** 2).sum()
+    torch.testing.assert_close(out[0], ref, rtol=1e-4, atol=1e-3)
+    assert out[1].item() == 0
+    x[5] = float("inf")
+    optim.sumsq_nonfinite_(x, out, accumulate=True)
+    assert out[1].item() == 1
+
+
+def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0):
+    torch.manual_seed(seed)
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device=DEV, dtype=torch.int32)
+    qkv = torch.randn(T, Hq + 2 * Hk, D, device=DEV, dtype=dtype)
+    q = qkv[:, :Hq].detach().requires_grad_(True)
+    k = qkv[:, Hq : Hq + Hk].detach().requires_grad_(True)
+    v = qkv[:, Hq + Hk :].detach().requires_grad_(True)
+    scale = 1 / math.sqrt(D)
+    o = attention.flash_attention(q, k, v, cu, cu, max(lens), max(lens), scale, causal, None if window < 0 else window)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = attention.attention_reference(qr, kr, vr, cu, cu, scale, causal, window)
+    torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float())
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        err = (a.grad.float() - b.grad).abs().max().item()
+        scl = b.grad.abs().max().item() + 1e-6
+        assert err / scl < 3e-2, (err, scl)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_basic(D, causal):
+    _attn_case([256], 4, 4, D, causal)
+
+
+def test_flash_attention_gqa_varlen():
+    _attn_case([100, 37, 300, 1], 8, 2, 128, True)
+
+
+def test_flash_attention_window():
+    _attn_case([333, 129], 4, 4, 64, True, window=50)
+
+
+def test_flash_attention_d32_noncausal_odd():
+    _attn_case([65, 7], 2, 1, 32, False)
+
+
+def test_flash_attention_deterministic():
+    torch.manual_seed(1)
+    T, H, D = 512, 4, 128
+    q, k, v = (torch.randn(T, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
+    g = torch.randn(T, H, D, device=DEV, dtype=torch.bfloat16)
+    grads = []
+    for _ in range(2):
+        for t in (q, k, v):
+            t.grad = None
+        attention.flash_attention(q, k, v, cu, cu, T, T, None, True).backward(g)
+        grads.append([t.grad.clone() for t in (q, k, v)])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
