@@ -57,7 +57,13 @@ def _common_flags(inc: list[str]) -> list[str]:
 
 
 def _sources() -> list[Path]:
-    return sorted(list(CSRC.rglob("*.hip")) + list(CSRC.rglob("*.cpp")))
+    """Sources of the torch/HIP extension ``_C`` (kernels + bindings)."""
+    return sorted(list((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp"])
+
+
+def _data_sources() -> list[Path]:
+    """Sources of the torch-free native data library ``_data``."""
+    return sorted((CSRC / "data").glob("*.cpp"))
 
 
 def _obj_for(src: Path, flags: list[str]) -> Path:
@@ -90,6 +96,38 @@ def ext_path() -> Path:
     return ROOT / "scaling_amd" / (EXT_NAME + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def data_ext_path() -> Path:
+    return ROOT / "scaling_amd" / ("_data" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_data(verbose: bool = True) -> Path:
+    """Build the pure C++ data-pipeline module (pybind11, no torch/HIP dependency)."""
+    import pybind11
+
+    BUILD.mkdir(parents=True, exist_ok=True)
+    srcs = _data_sources()
+    flags = ["-O3", "-fPIC", "-std=c++17", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    objs = []
+    for src in srcs:
+        obj = _obj_for(src, flags)
+        if not obj.exists():
+            cmd = [os.environ.get("CXX", "g++")] + flags + ["-c", str(src), "-o", str(obj) + ".tmp"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {src}\n{r.stderr}")
+            os.replace(str(obj) + ".tmp", obj)
+        objs.append(obj)
+    out = data_ext_path()
+    cmd = [os.environ.get("CXX", "g++"), "-shared", "-fPIC", "-o", str(out) + ".tmp"] + [str(o) for o in objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{r.stderr}")
+    os.replace(str(out) + ".tmp", out)
+    if verbose:
+        print(f"[scaling_amd] built {out.name}", file=sys.stderr)
+    return out
+
+
 def build(verbose: bool = True, jobs: int | None = None) -> Path:
     inc, lib = _torch_paths()
     flags = _common_flags(inc)
@@ -119,5 +157,10 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     return out
 
 
+def build_all(verbose: bool = True) -> None:
+    build_data(verbose)
+    build(verbose)
+
+
 if __name__ == "__main__":
-    build()
+    build_all()

@@ -1,0 +1,395 @@
+"""Tensor-parallel self-attention (reference ``src/scaling/core/nn/attention/attention.py:268-796``).
+
+Same constructor, parameter names (``query_key_value`` or ``query``/``key``/``value``, ``dense``,
+LoRA ``lora_modules``, ``norm_query``/``norm_key``) and forward signature.  Internals are
+MI355X-first:
+
+* activations stay token-major: the projection output ``[b, s, heads*hd]`` *is* ``[T, heads, hd]``,
+  so q/k/v are strided views (no ``rearrange`` copies); separate q/k/v weights run as ONE GEMM
+  (``fused_column_linear``) with one TP all-reduce in backward;
+* RoPE is a HIP kernel applied on those views; attention is the HIP flash kernel (varlen
+  ``cu_seqlens``, causal, sliding window incl. mixed local/global heads, GQA without ``repeat_kv``);
+* the ``torch`` kernel keeps the reference's dense masked-softmax math (needed for
+  attention-score manipulation / AtMan).
+"""
+from __future__ import annotations
+
+import math
+from enum import Enum
+from typing import Callable, Optional, Union
+
+import torch
+
+from ....ops import attention as attn_ops
+from ...topology import Topology
+from ..linear import ColumnParallelLinear, RowParallelLinear
+from ..linear.fused import fused_column_linear
+from ..linear.utils import all_concat, all_reduce_scatter_to_sequence_parallel, all_shard
+from ..lora import ParallelLoRa
+from ..lora_config import LoRaConfig, LoRAModuleType
+from ..masked_softmax import MaskedSoftmax, MaskedSoftmaxConfig, MaskedSoftmaxKernel
+from ..norm import LayerNorm, LayerNormConfig, NormType, RMSNorm, get_norm
+from ..rotary import RotaryConfig, RotaryEmbedding, RotaryEmbeddingComplex
+
+
+class RelativePositionEmbeddingType(Enum):
+    NONE = "none"
+    ROTARY = "rotary"
+    ROTARY_COMPLEX = "rotary_complex"
+
+
+def split_tensor_along_last_dim(tensor: torch.Tensor, num_partitions: int) -> tuple[torch.Tensor, ...]:
+    return tuple(torch.split(tensor, tensor.shape[-1] // num_partitions, dim=-1))
+
+
+def repeat_kv(x: torch.Tensor, n_rep: int) -> torch.Tensor:
+    if n_rep == 1:
+        return x
+    return x.repeat_interleave(n_rep, dim=-2)
+
+
+def get_max_seq_length(cumulative_seq_lengths: torch.Tensor) -> int:
+    return int((cumulative_seq_lengths[1:] - cumulative_seq_lengths[:-1]).max().item())
+
+
+def _segment_ids(cu: torch.Tensor, total: int) -> torch.Tensor:
+    ids = torch.zeros(total, dtype=torch.long, device=cu.device)
+    if cu.numel() > 2:
+        ids.index_add_(0, cu[1:-1].long(), torch.ones(cu.numel() - 2, dtype=torch.long, device=cu.device))
+    return ids.cumsum(0)
+
+
+def cumulative_seq_lengths_to_dense_attention_mask(
+    cumulative_seq_lengths: torch.Tensor, seq_length_per_batch_item: int, causal: bool
+) -> torch.Tensor:
+    """Boolean mask [b, 1, s, s], True = masked (reference ``attention.py:69-93``), vectorised."""
+    total = int(cumulative_seq_lengths[-1].item())
+    b = total // seq_length_per_batch_item
+    seg = _segment_ids(cumulative_seq_lengths, total).view(b, seq_length_per_batch_item)
+    allowed = seg[:, :, None] == seg[:, None, :]
+    if causal:
+        allowed = torch.tril(allowed)
+    return ~allowed.unsqueeze(1)
+
+
+def multi_head_attention(
+    query: torch.Tensor,
+    key: torch.Tensor,
+    value: torch.Tensor,
+    cumulative_seq_lengths: torch.Tensor,
+    causal: bool,
+    query_key_scaling_factor: float,
+    softmax_fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
+    dropout_fn: Optional[Callable[[torch.Tensor], torch.Tensor]] = None,
+    attention_scores_manipulation: Optional[torch.Tensor] = None,
+    attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True,
+    use_matmul: bool = False,
+    cumulative_seq_lengths_key: Optional[torch.Tensor] = None,
+) -> torch.Tensor:
+    """Dense attention on [b, s, n, hd] tensors (k/v already repeated to n heads). Returns [b, s, n*hd]."""
+    b, sq, n, hd = query.shape
+    sk = key.shape[1]
+    q = query.transpose(1, 2)
+    k = key.transpose(1, 2)
+    v = value.transpose(1, 2)
+    scores = torch.matmul(q, k.transpose(-1, -2)) * query_key_scaling_factor  # [b, n, sq, sk]
+    if cumulative_seq_lengths_key is None and sq == sk:
+        mask = cumulative_seq_lengths_to_dense_attention_mask(cumulative_seq_lengths, sq, causal)
+    else:
+        # cached decoding: one query block attending to all keys (bottom-right causal alignment)
+        qpos = torch.arange(sq, device=q.device)[:, None] + (sk - sq)
+        kpos = torch.arange(sk, device=q.device)[None, :]
+        mask = (kpos > qpos) if causal else torch.zeros(sq, sk, dtype=torch.bool, device=q.device)
+        mask = mask[None, None].expand(b, 1, sq, sk)
+    if attention_scores_manipulation is not None:
+        flags = (
+            [attentions_score_manipulation_log_additive] * b
+            if isinstance(attentions_score_manipulation_log_additive, bool)
+            else list(attentions_score_manipulation_log_additive)
+        )
+        rows = []
+        for i in range(b):
+            si = scores[i]
+            if flags[i]:
+                si = si + attention_scores_manipulation[i]
+            else:
+                shift = si.masked_fill(mask[i], 10000.0).min(-1).values.unsqueeze(-1)
+                si = (si - shift) * attention_scores_manipulation[i]
+            rows.append(si)
+        scores = torch.stack(rows)
+    probs = softmax_fn(scores, mask)
+    if dropout_fn is not None:
+        probs = dropout_fn(probs)
+    out = torch.matmul(probs.to(v.dtype), v)  # [b, n, sq, hd]
+    return out.transpose(1, 2).reshape(b, sq, n * hd)
+
+
+class ParallelSelfAttention(torch.nn.Module):
+    def __init__(
+        self,
+        hidden_size: int,
+        num_attention_heads: int,
+        masked_softmax_config: MaskedSoftmaxConfig,
+        causal: bool = True,
+        num_local_attention_heads: int = 0,
+        local_attention_window_size: Optional[int] = None,
+        scaling_factor: Optional[float] = None,
+        dropout_attention_probs: float = 0.0,
+        rotary_config: Optional[RotaryConfig] = None,
+        relative_position_embedding_type: RelativePositionEmbeddingType = RelativePositionEmbeddingType.ROTARY,
+        bias: bool = True,
+        device: Optional[torch.device] = None,
+        dtype: torch.dtype = torch.float32,
+        topology: Optional[Topology] = None,
+        init_method: Callable[[torch.Tensor], torch.Tensor] = torch.nn.init.xavier_normal_,
+        bitfit_bias_name: Optional[str] = None,
+        lora_config: Optional[LoRaConfig] = None,
+        norm_type: NormType = NormType.LAYERNORM,
+        key_query_norm: bool = False,
+        layernorm_config: Optional[LayerNormConfig] = None,
+        qkv_in_one: bool = True,
+        num_kv_heads: Optional[int] = None,
+        use_matmul: bool = False,
+    ) -> None:
+        super().__init__()
+        assert not (topology is not None and device is not None), "cannot specify both device and topology"
+        from ..linear.utils import get_device
+
+        self._device = get_device(topology=topology, device=device)
+        assert hidden_size % num_attention_heads == 0, "hidden size must be divisible by num_attention_heads"
+        self.hidden_size = hidden_size
+        self.hidden_size_per_attention_head = hidden_size // num_attention_heads
+        self.num_attention_heads = num_attention_heads
+        self.causal = causal
+        self.lora_config = lora_config
+        self.use_flash_attention = masked_softmax_config.kernel == MaskedSoftmaxKernel.FLASH_ATTENTION
+        self.masked_softmax_config = masked_softmax_config
+        self.num_local_attention_heads = num_local_attention_heads
+        self.local_attention_window_size = local_attention_window_size
+        mp = 1 if topology is None else topology.config.model_parallel_size
+        if num_local_attention_heads > 0:
+            assert self.use_flash_attention, "local attention is currently only supported with `flash_attention`."
+            assert local_attention_window_size is not None, "`local_attention_window_size` needs to be set"
+            if num_local_attention_heads != num_attention_heads and mp > 1:
+                raise NotImplementedError("Mixed range attention is not supported with tensor parallelism.")
+        assert num_attention_heads % mp == 0, "attention heads must be divisible by model parallel size"
+        self.num_attention_heads_per_partition = num_attention_heads // mp
+        self.dtype = dtype
+        self.qkv_in_one = qkv_in_one
+        self.num_kv_heads = num_kv_heads
+        if num_kv_heads:
+            assert not qkv_in_one, "for a differing number of kv heads, qkv cannot be stored in one"
+            self.num_kv_heads_per_partition = num_kv_heads // mp
+            self.num_repeat_kv = self.num_attention_heads_per_partition // self.num_kv_heads_per_partition
+        else:
+            self.num_kv_heads_per_partition = self.num_attention_heads_per_partition
+            self.num_repeat_kv = 1
+        if lora_config:
+            self.lora_merged_state = False
+            self.lora_modules = torch.nn.ModuleDict()
+            for mt in lora_config.parallel_modules:
+                rep = 1 if mt in (LoRAModuleType.DENSE, LoRAModuleType.QUERY) else self.num_repeat_kv
+                self.lora_modules[f"{mt.value}_{lora_config.name}"] = ParallelLoRa(
+                    in_features=hidden_size,
+                    out_features=hidden_size // rep,
+                    rank=lora_config.rank,
+                    topology=topology,
+                    dropout=lora_config.dropout,
+                    dtype=dtype,
+                    lora_module_type=mt,
+                    alpha=lora_config.alpha,
+                    bias=lora_config.bias,
+                    kaiming_a=lora_config.kaiming_a,
+                )
+        kw = dict(bias=bias, device=device, dtype=dtype, topology=topology, init_method=init_method,
+                  bitfit_bias_name=bitfit_bias_name, parallel_output=True)
+        if qkv_in_one:
+            self.query_key_value = ColumnParallelLinear(hidden_size, 3 * hidden_size, **kw)
+        else:
+            self.query = ColumnParallelLinear(hidden_size, hidden_size, **kw)
+            self.key = ColumnParallelLinear(hidden_size, hidden_size // self.num_repeat_kv, **kw)
+            self.value = ColumnParallelLinear(hidden_size, hidden_size // self.num_repeat_kv, **kw)
+        self.use_matmul = use_matmul
+        self.scaling_factor = (
+            scaling_factor if scaling_factor is not None else 1 / math.sqrt(self.hidden_size_per_attention_head)
+        )
+        self.rotary_embedding: Optional[Union[RotaryEmbedding, RotaryEmbeddingComplex]] = None
+        if relative_position_embedding_type == RelativePositionEmbeddingType.ROTARY:
+            assert rotary_config is not None
+            self.rotary_embedding = RotaryEmbedding(rotary_config, device=self._device, dtype=dtype)
+        elif relative_position_embedding_type == RelativePositionEmbeddingType.ROTARY_COMPLEX:
+            assert rotary_config is not None
+            self.rotary_embedding = RotaryEmbeddingComplex(rotary_config, device=self._device)
+        elif relative_position_embedding_type != RelativePositionEmbeddingType.NONE:
+            raise NotImplementedError
+        self.key_query_norm = key_query_norm
+        self.topology = topology
+        self.norm_query: Optional[Union[LayerNorm, RMSNorm]] = None
+        self.norm_key: Optional[Union[LayerNorm, RMSNorm]] = None
+        if key_query_norm:
+            self.norm_query = get_norm(norm_type, layernorm_config, self.hidden_size_per_attention_head,
+                                       self._device, dtype, bitfit_bias_name)
+            self.norm_key = get_norm(norm_type, layernorm_config, self.hidden_size_per_attention_head,
+                                     self._device, dtype, bitfit_bias_name)
+        self.dropout_attention_probs = dropout_attention_probs
+        self.dropout = torch.nn.Dropout(dropout_attention_probs)
+        self.dense = RowParallelLinear(
+            hidden_size, hidden_size, bias=bias, topology=topology, dtype=dtype, device=device,
+            bitfit_bias_name=bitfit_bias_name, init_method=init_method, parallel_input=True,
+            parallel_output=(topology.config.sequence_parallel if topology is not None else False),
+        )
+        self.masked_softmax = MaskedSoftmax(config=masked_softmax_config)
+        self.cache: dict[int, tuple[Optional[torch.Tensor], Optional[torch.Tensor]]] = {}
+
+    # ------------------------------------------------------------------ projections
+    def _project(self, x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Returns token-major q [T, nq, hd], k/v [T, nkv, hd] (possibly strided views)."""
+        b, s, _ = x.shape
+        T = b * s
+        hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
+        if self.qkv_in_one:
+            qkv = self.query_key_value(x).view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
+            return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :]
+        out = fused_column_linear(x, [self.query, self.key, self.value], self.topology)
+        out = out.view(T, nq * hd + 2 * nkv * hd)
+        q = out[:, : nq * hd].view(T, nq, hd)
+        k = out[:, nq * hd : (nq + nkv) * hd].view(T, nkv, hd)
+        v = out[:, (nq + nkv) * hd :].view(T, nkv, hd)
+        return q, k, v
+
+    def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
+        assert self.lora_config is not None
+        T = x.shape[0] * x.shape[1]
+        for name, mod in self.lora_modules.items():
+            if name == f"dense_{self.lora_config.name}":
+                continue
+            out = mod(x).reshape(T, -1, self.hidden_size_per_attention_head)
+            if mod.lora_module_type == LoRAModuleType.QUERY:
+                query = query + out
+            elif mod.lora_module_type == LoRAModuleType.KEY:
+                key = key + out
+            elif mod.lora_module_type == LoRAModuleType.VALUE:
+                value = value + out
+        return [query, key, value]
+
+    # ------------------------------------------------------------------ forward
+    def forward(
+        self,
+        x: torch.Tensor,
+        cumulative_seq_lengths: torch.Tensor,
+        position_ids: Optional[torch.Tensor],
+        cumulative_seq_lengths_key: Optional[torch.Tensor] = None,
+        use_cache: bool = False,
+        reset_cache: bool = False,
+        cache_index: int = 0,
+        attention_scores_manipulation: Optional[torch.Tensor] = None,
+        attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True,
+        max_seq_length: Optional[int] = None,
+    ) -> torch.Tensor:
+        b, s, _ = x.shape
+        T = b * s
+        hd = self.hidden_size_per_attention_head
+        q, k, v = self._project(x)
+        if self.lora_config is not None and not self.lora_merged_state:
+            q, k, v = self.apply_lora(x, q, k, v)
+        if self.key_query_norm:
+            assert self.norm_query is not None and self.norm_key is not None
+            q = all_shard(self.norm_query(all_concat(q, dim=1, topology=self.topology)), dim=1, topology=self.topology)
+            k = all_shard(self.norm_key(all_concat(k, dim=1, topology=self.topology)), dim=1, topology=self.topology)
+        if self.rotary_embedding is not None:
+            pos = position_ids.reshape(-1) if position_ids is not None else None
+            q = self.rotary_embedding.apply_tokens(q, pos, s)
+            k = self.rotary_embedding.apply_tokens(k, pos, s)
+
+        if use_cache:
+            if not self.causal:
+                raise ValueError("KV caching is only supported for causal attention.")
+            assert b == 1, f"KV caching is only supported for batch size 1, got {b}"
+            if reset_cache:
+                self.cache[cache_index] = (k, v)
+            else:
+                pk, pv = self.cache[cache_index]
+                assert pk is not None and pv is not None
+                k = torch.cat((pk, k), dim=0)
+                v = torch.cat((pv, v), dim=0)
+                self.cache[cache_index] = (k, v)
+            cumulative_seq_lengths_key = torch.tensor([0, k.shape[0]], device=x.device, dtype=torch.int32)
+        elif reset_cache:
+            self.cache[cache_index] = (None, None)
+
+        Tk = k.shape[0]
+        if self.use_flash_attention:
+            cu_k = cumulative_seq_lengths_key if cumulative_seq_lengths_key is not None else cumulative_seq_lengths
+            # segments never cross a batch row, so the row length bounds every segment: no host sync
+            max_q = max_seq_length if max_seq_length is not None else s
+            max_k = max_q if cumulative_seq_lengths_key is None else Tk
+            nl = self.num_local_attention_heads
+            common = dict(
+                cu_seqlens_q=cumulative_seq_lengths, cu_seqlens_k=cu_k, max_seqlen_q=max_q, max_seqlen_k=max_k,
+                softmax_scale=self.scaling_factor, causal=self.causal, dropout_p=self.dropout_attention_probs,
+                training=self.training,
+            )
+            if nl <= 0 or nl == self.num_attention_heads:
+                window = self.local_attention_window_size if nl > 0 else None
+                hidden = attn_ops.flash_attention(q, k, v, window=window, **common)
+            else:
+                rep = self.num_repeat_kv
+                kr, vr = repeat_kv(k, rep), repeat_kv(v, rep)
+                h_loc = attn_ops.flash_attention(q[:, :nl], kr[:, :nl], vr[:, :nl],
+                                                 window=self.local_attention_window_size, **common)
+                h_glob = attn_ops.flash_attention(q[:, nl:], kr[:, nl:], vr[:, nl:], window=None, **common)
+                hidden = torch.cat([h_loc, h_glob], dim=1)
+            hidden = hidden.reshape(b, s, -1)
+        else:
+            kr = repeat_kv(k, self.num_repeat_kv).reshape(b, Tk // b, -1, hd)
+            vr = repeat_kv(v, self.num_repeat_kv).reshape(b, Tk // b, -1, hd)
+            hidden = multi_head_attention(
+                q.reshape(b, s, -1, hd), kr, vr, cumulative_seq_lengths, self.causal, self.scaling_factor,
+                softmax_fn=self.masked_softmax, dropout_fn=self.dropout,
+                attention_scores_manipulation=attention_scores_manipulation,
+                attentions_score_manipulation_log_additive=attentions_score_manipulation_log_additive,
+                use_matmul=self.use_matmul,
+                cumulative_seq_lengths_key=None if Tk == T else cumulative_seq_lengths_key,
+            )
+
+        dense_lora = None
+        if self.lora_config and not self.lora_merged_state and LoRAModuleType.DENSE in self.lora_config.parallel_modules:
+            dense_lora = self.lora_modules[f"dense_{self.lora_config.name}"](
+                all_concat(hidden, dim=-1, topology=self.topology)
+            )
+        out = self.dense(hidden)
+        if dense_lora is not None:
+            out = out + dense_lora
+        if self.topology is not None and self.topology.config.sequence_parallel:
+            out = all_reduce_scatter_to_sequence_parallel(out, self.topology)
+        return out
+
+    # ------------------------------------------------------------------ LoRA merge
+    def _get_delta_one_q_k_v(self) -> torch.Tensor:
+        assert self.lora_config is not None
+        w = self.query_key_value.weight
+        nq = self.num_attention_heads_per_partition
+        hd = self.hidden_size_per_attention_head
+        delta = torch.zeros(nq, 3, hd, w.shape[1], dtype=w.dtype, device=w.device)
+        idx = {f"query_{self.lora_config.name}": 0, f"key_{self.lora_config.name}": 1, f"value_{self.lora_config.name}": 2}
+        for name, mod in self.lora_modules.items():
+            if name in idx:
+                delta[:, idx[name]] += mod.get_delta_weights().view(nq, hd, -1).to(w.dtype)
+        return delta.view_as(w)
+
+    @torch.no_grad()
+    def merge_lora_weights(self) -> None:
+        assert self.lora_config and self.lora_modules, "Merge of LoRa weights called without proper configuration."
+        if self.qkv_in_one:
+            keys = {f"{m.value}_{self.lora_config.name}" for m in (LoRAModuleType.KEY, LoRAModuleType.VALUE, LoRAModuleType.QUERY)}
+            if keys.intersection(self.lora_modules.keys()):
+                self.query_key_value.weight.data += self._get_delta_one_q_k_v()
+        else:
+            for name, mod in self.lora_modules.items():
+                target = name.split("_")[0]
+                if target != "dense":
+                    getattr(self, target).weight.data += mod.get_delta_weights().to(self.dtype)
+        if LoRAModuleType.DENSE in self.lora_config.parallel_modules:
+            self.dense.weight.data += self.lora_modules[f"dense_{self.lora_config.name}"].get_delta_weights().to(self.dtype)
+        del self.lora_modules
+        self.lora_merged_state = True

@@ -1,0 +1,53 @@
+"""Activation checkpointing that also replays the model-parallel-constant RNG stream.
+
+Parity: reference ``activation_checkpointing.py:72-190`` (non-reentrant checkpoint that snapshots
+and restores the Topology RNG tracker so recomputed dropout matches).  Built on the public
+``torch.utils.checkpoint(use_reentrant=False, context_fn=...)`` API; torch's own
+``preserve_rng_state`` covers the global CPU/HIP generators.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Any, Callable, Iterator
+
+import torch
+from torch.utils.checkpoint import checkpoint
+
+
+def _tracker_contexts(topology: Any) -> tuple:
+    tracker = getattr(topology, "_model_parallel_constant_rng", None)
+    saved: dict[str, Any] = {}
+
+    @contextlib.contextmanager
+    def forward_ctx() -> Iterator[None]:
+        if tracker is not None:
+            saved["state"] = tracker.state.clone()
+        yield
+
+    @contextlib.contextmanager
+    def recompute_ctx() -> Iterator[None]:
+        if tracker is None or "state" not in saved:
+            yield
+            return
+        current = tracker.state
+        tracker.state = saved["state"].clone()
+        try:
+            yield
+        finally:
+            tracker.state = current
+
+    return forward_ctx(), recompute_ctx()
+
+
+def checkpoint_with_rng(function: Callable[..., Any], topology: Any, preserve_rng_state: bool, *args: Any) -> Any:
+    return checkpoint(
+        function,
+        *args,
+        use_reentrant=False,
+        preserve_rng_state=preserve_rng_state,
+        context_fn=lambda: _tracker_contexts(topology),
+    )
+
+
+# reference-compatible name
+_checkpoint_without_reentrant = checkpoint_with_rng

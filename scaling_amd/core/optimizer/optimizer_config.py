@@ -1,0 +1,28 @@
+from pydantic import Field
+
+from ..config import BaseConfig
+from .loss_scaler_config import LossScalerConfig
+
+
+class OptimizerConfig(BaseConfig):
+    method: str = Field("adamw", description="Which optimization method to use.")
+    beta1: float = Field(0.9, description="AdamW beta1")
+    beta2: float = Field(0.95, description="AdamW beta2")
+    eps: float = Field(1e-8, description="AdamW epsilon")
+    gradient_clipping: float = Field(1.0, description="clip global l2 grads to this value, deactivate if 0.0", ge=0.0)
+    allreduce_bucket_size: int = Field(500000000, description="upper bound of elements per gradient bucket", gt=0)
+    loss_scaler: LossScalerConfig = Field(LossScalerConfig(), description="Configuration of the loss scaler")
+    zero: bool = Field(False, description="enable ZeRO stage 1 (optimizer state sharded over data parallel)")
+    zero_save_static: bool = Field(False, description="save per-rank optimizer files instead of merged per-layer files")
+    debug_log: bool = Field(False)
+    # --- MI355X-native additions (optional) ---
+    grad_bucket_numel: int = Field(
+        2**26,
+        description="elements per gradient communication bucket (reduce-scatter / all-gather granularity); "
+        "buckets are launched on a side stream as soon as their grads are final (overlap with backward)",
+        gt=0,
+    )
+    grad_reduce_dtype: str = Field(
+        "float32", description="dtype of the data-parallel gradient reduction ('float32' as the reference, or 'bfloat16')"
+    )
+    overlap_grad_reduce: bool = Field(True, description="overlap the data-parallel gradient reduction with backward")

@@ -1,0 +1,32 @@
+from pathlib import Path
+from typing import Optional
+
+from pydantic import Field
+
+from ..config import BaseConfig
+
+
+class TrainerConfig(BaseConfig):
+    save_dir: Optional[Path] = Field(None, description="directory for saving checkpoints")
+    save_interval: Optional[int] = Field(None, description="save a checkpoint every 'save_interval' steps")
+    load_dir: Optional[Path] = Field(None, description="directory for loading checkpoints")
+    train_iterations: Optional[int] = Field(None, description="train for this number of iterations")
+    assert_checkpoint_loaded: bool = Field(True, description="error out if a checkpoint could not be loaded")
+    load_optimizer_states: bool = Field(True, description="load optimizer states on checkpoint load")
+    delete_past_optimizer_states: bool = Field(
+        True, description="delete optimizer states of older checkpoints after saving a new one (Determined only)"
+    )
+    load_context: bool = Field(True, description="load iterations / consumed samples / RNG on checkpoint load")
+    allowed_missing_keys_in_checkpoint: Optional[list[str]] = Field(None, description="regexes of parameters that may be missing")
+    allowed_unexpected_keys_in_checkpoint: Optional[list[str]] = Field(None, description="regexes of extra checkpoint keys to ignore")
+    ignore_keys_in_checkpoint: Optional[list[str]] = Field(None, description="regexes of checkpoint keys not to load")
+    merge_lora_after_loading_checkpoint: Optional[bool] = Field(False, description="merge LoRA weights after loading")
+    seed: int = Field(42, description="")
+    dataloader_num_workers: int = Field(0, description="")
+    dataloader_pin_memory: bool = Field(True, description="")
+    dataloader_prefetch_factor: Optional[int] = Field(None, description="")
+    eval_iterations: int = Field(1, description="(not implemented in the reference either: one eval step)")
+    eval_interval: Optional[int] = Field(None, description="evaluate every eval_interval steps")
+    separate_file_for_parameters: Optional[list[str]] = Field(
+        None, description="create a separate checkpoint file for parameters matching these names"
+    )

@@ -1,0 +1,135 @@
+"""Pre-norm transformer block (reference ``model/layers/layer.py:44-291``): attention block and MLP
+block with residuals, dropouts under the TP-constant RNG, optional bottleneck adapters."""
+from __future__ import annotations
+
+from functools import partial
+from typing import Callable, Optional, Union
+
+import torch
+
+from ....core import ParallelMLP, ParallelSelfAttention, ParallelSwiGLUMLP, RotaryConfig, Topology, get_norm
+from ...context.config import MLPType, TransformerArchitectureConfig
+from .base import TransformerLayerBaseIO, TransformerLayerIO
+from .embedding import _device
+
+
+class ZeroLayer(torch.nn.Module):
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.zeros_like(x)
+
+
+def get_batched_adapter_forward(adapter_list: list[Optional[torch.nn.Module]]) -> Callable[[torch.Tensor], torch.Tensor]:
+    mods = [a if a is not None else ZeroLayer() for a in adapter_list]
+
+    def forward(x: torch.Tensor) -> torch.Tensor:
+        assert x.shape[0] == len(mods)
+        return torch.stack([m(x[i]) for i, m in enumerate(mods)], dim=0)
+
+    return forward
+
+
+class TransformerLayer(TransformerLayerBaseIO):
+    def __init__(self, architecture_config: TransformerArchitectureConfig, layer_index: int,
+                 topology: Optional[Topology] = None,
+                 init_method: Callable[[torch.Tensor], torch.Tensor] = torch.nn.init.xavier_normal_) -> None:
+        super().__init__()
+        cfg = architecture_config
+        self.architecture_config = cfg
+        self.topology = topology
+        self.layer_index = layer_index
+        dev = _device(topology)
+        bitfit = getattr(cfg.bitfit_bias_config, "name", None)
+        dtype = cfg.precision.dtype
+        self.input_layernorm = get_norm(cfg.norm_type, cfg.layernorm, cfg.hidden_size, dev, dtype, bitfit, topology)
+        head_dim = cfg.hidden_size // cfg.num_attention_heads
+        self.self_attention = ParallelSelfAttention(
+            hidden_size=cfg.hidden_size, num_attention_heads=cfg.num_attention_heads,
+            num_local_attention_heads=cfg.num_local_attention_heads,
+            local_attention_window_size=cfg.local_attention_window_size, masked_softmax_config=cfg.masked_softmax,
+            causal=cfg.causal, dropout_attention_probs=cfg.dropout_attention_probs,
+            rotary_config=RotaryConfig(dimensions=int(cfg.rotary_percentage * head_dim), max_seq_length=cfg.sequence_length,
+                                       base=cfg.rotary_embedding_base),
+            relative_position_embedding_type=cfg.relative_position_embedding_type, bias=cfg.attention_bias,
+            topology=topology, device=None if topology is not None else dev, dtype=dtype, bitfit_bias_name=bitfit,
+            init_method=init_method, lora_config=cfg.lora_config, norm_type=cfg.norm_type, key_query_norm=cfg.key_query_norm,
+            layernorm_config=cfg.layernorm, qkv_in_one=cfg.attention_qkv_in_one, num_kv_heads=cfg.attention_num_kv_heads,
+            use_matmul=cfg.attention_use_matmul,
+        )
+        self.dropout_attention = torch.nn.Dropout(cfg.dropout_after_attention)
+        self.post_attention_layernorm = get_norm(cfg.norm_type, cfg.layernorm, cfg.hidden_size, dev, dtype, bitfit, topology)
+        mlp_kw = dict(io_features=cfg.hidden_size, intermediate_feature_factor=cfg.mlp_factor, bias=cfg.mlp_bias,
+                      topology=topology, device=None if topology is not None else dev, dtype=dtype,
+                      bitfit_bias_name=bitfit, init_method=init_method)
+        self.mlp: Union[ParallelMLP, ParallelSwiGLUMLP]
+        if cfg.mlp_type == MLPType.DEFAULT:
+            self.mlp = ParallelMLP(**mlp_kw)
+        elif cfg.mlp_type == MLPType.SWIGLU:
+            self.mlp = ParallelSwiGLUMLP(**mlp_kw)
+        else:
+            raise NotImplementedError(str(cfg.mlp_type))
+        self.dropout_mlp = torch.nn.Dropout(cfg.dropout_after_mlp)
+        if cfg.adapter_config is not None:
+            self.load_adapter()
+
+    def load_adapter(self) -> None:
+        ac = self.architecture_config.adapter_config
+        assert ac is not None
+        dev = _device(self.topology)
+        kw = dict(io_features=self.architecture_config.hidden_size, bias=False, topology=self.topology,
+                  device=None if self.topology is not None else dev, dtype=self.architecture_config.precision.dtype,
+                  init_method=partial(torch.nn.init.normal_, mean=0.0, std=ac.init_std))
+        if ac.attention_downsampling_factor is not None:
+            self.attn_adapter_name = f"attn_adapter_{ac.name}"
+            setattr(self, self.attn_adapter_name, ParallelMLP(intermediate_feature_factor=ac.attention_downsampling_factor, **kw))
+        if ac.mlp_downsampling_factor is not None:
+            self.mlp_adapter_name = f"mlp_adapter_{ac.name}"
+            setattr(self, self.mlp_adapter_name, ParallelMLP(intermediate_feature_factor=ac.mlp_downsampling_factor, **kw))
+
+    def apply_adapter(self, x: torch.Tensor, adapter_name: str) -> torch.Tensor:
+        assert hasattr(self, adapter_name), f"cannot use adapter '{adapter_name}' as it is not initialized"
+        return getattr(self, adapter_name)(x)
+
+    def _dropout(self, drop: torch.nn.Dropout, x: torch.Tensor) -> torch.Tensor:
+        if drop.p == 0.0 or not self.training:
+            return x
+        if self.topology is not None:
+            with self.topology.model_parallel_constant_rng():
+                return drop(x)
+        return drop(x)
+
+    def attention_block(self, hidden_state: torch.Tensor, cumulative_seq_lengths: torch.Tensor, position_ids: torch.Tensor,
+                        use_cache: bool = False, reset_cache: bool = False, cache_index: int = 0,
+                        attention_scores_manipulation: Optional[torch.Tensor] = None,
+                        attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True) -> torch.Tensor:
+        h = self.input_layernorm(hidden_state)
+        h = self.self_attention(
+            h, cumulative_seq_lengths=cumulative_seq_lengths, position_ids=position_ids, use_cache=use_cache,
+            reset_cache=reset_cache, cache_index=cache_index, attention_scores_manipulation=attention_scores_manipulation,
+            attentions_score_manipulation_log_additive=attentions_score_manipulation_log_additive,
+        )
+        out = hidden_state + self._dropout(self.dropout_attention, h)
+        if hasattr(self, "attn_adapter_name"):
+            out = out + self.apply_adapter(out, self.attn_adapter_name)
+        return out
+
+    def mlp_block(self, hidden_state: torch.Tensor) -> torch.Tensor:
+        h = self.mlp(self.post_attention_layernorm(hidden_state))
+        out = hidden_state + self._dropout(self.dropout_mlp, h)
+        if hasattr(self, "mlp_adapter_name"):
+            out = out + self.apply_adapter(out, self.mlp_adapter_name)
+        return out
+
+    def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
+        st = x.inference_settings
+        assert x.cumulative_seq_lengths is not None
+        act = self.attention_block(
+            x.activations, x.cumulative_seq_lengths, x.position_ids,
+            use_cache=st.use_cache if st else False, reset_cache=st.reset_cache if st else False,
+            cache_index=st.cache_index if st else 0, attention_scores_manipulation=x.attention_scores_manipulation,
+            attentions_score_manipulation_log_additive=st.control_log_additive_batch if st else True,
+        )
+        act = self.mlp_block(act)
+        if st is not None and (self.layer_index + 1) in st.embedding_layers:
+            assert x.embeddings is not None
+            x.embeddings[st.embedding_layers.index(self.layer_index + 1)] = act
+        return x.derive(act, embeddings_head=None)

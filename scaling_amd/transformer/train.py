@@ -1,0 +1,182 @@
+"""Training entry point (reference ``transformer/train.py``): config → topology → context → model →
+optimizer → datasets → ``TransformerTrainer.run_training``.
+
+Run one process per GPU, e.g. ``python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1
+-m scaling_amd.transformer.train --payload <base64 config>`` or via ``scaling_amd.core.runner``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+from pathlib import Path
+from typing import Any, Callable, Optional
+
+import torch
+
+from ..core import BaseBlendedDataset, BaseDataset, DeterminedBaseTrainer, Topology
+from ..core.logging import logger
+from ..core.nn.parallel_module import EvaluationStepOutput, TrainStepOutput
+from ..core.runner.launch_config import LaunchConfig
+from .context import TransformerConfig, TransformerContext
+from .context.config import DataConfig
+from .data.text_dataset import TextBlendedDataset, TextDataset
+from .dataset_loader import load_datasets
+from .model import TransformerParallelModule, init_model, init_optimizer
+from .model.model import loss_function, metrics_aggregation_fn
+from .utils.get_tflops import (
+    get_model_flop_utilization_palm,
+    get_tflops_aleph_alpha,
+    get_tflops_bloom,
+    get_tflops_electra,
+    get_tflops_megatron,
+    get_tokens_per_second,
+)
+
+
+class TransformerTrainer(DeterminedBaseTrainer[TransformerContext, TransformerParallelModule]):
+    def save_checkpoint(self, save_dir: Optional[Path] = None) -> Path:
+        save_dir = super().save_checkpoint(save_dir=save_dir)
+        vocab = self.context.config.transformer_architecture.vocab_file
+        if vocab is not None and save_dir is not None:
+            shutil.copy(vocab, Path(save_dir) / "vocab.json")
+        return save_dir
+
+    def log_metrics(self, train_step_output: TrainStepOutput,
+                    eval_step_output: Optional[EvaluationStepOutput] = None) -> dict[str, Any]:
+        logger.info(f"completed step {self.context.iterations}")
+        m = self._train_metrics(train_step_output)
+        m |= self._tflops_metrics(self.parameters_total, self.parameters_unique, train_step_output.step_duration)
+        if eval_step_output is not None:
+            m |= {f"evaluation/{k}": v for k, v in (eval_step_output.metrics or {}).items()}
+            m["evaluation/loss"] = eval_step_output.loss
+            m["evaluation/step_duration"] = eval_step_output.step_duration
+        logger.log_metrics(m, step=self.context.iterations)
+        return m
+
+    def _tflops_metrics(self, parameter_count: int, parameter_count_unique: int, iter_time_s: float) -> dict[str, float]:
+        a, t = self.context.config.transformer_architecture, self.context.topology
+        return {
+            "runtime/tflops_megatron": get_tflops_megatron(parameter_count, iter_time_s, t, a),
+            "runtime/tflops_megatron_layout_independent": get_tflops_megatron(parameter_count_unique, iter_time_s, t, a),
+            "runtime/tflops_bloom": get_tflops_bloom(iter_time_s, t, a),
+            "runtime/tflops_electra": get_tflops_electra(iter_time_s, t, a),
+            "runtime/tflops_aleph_alpha": get_tflops_aleph_alpha(iter_time_s, t, a),
+            "runtime/mfu_palm": get_model_flop_utilization_palm(iter_time_s, parameter_count, t, a),
+            "runtime/tokens_per_second": get_tokens_per_second(iter_time_s, t, a),
+        }
+
+    @staticmethod
+    def _train_metrics(tso: TrainStepOutput) -> dict[str, Any]:
+        m: dict[str, Any] = {"training/loss": tso.loss, "runtime/step_duration": tso.step_duration}
+        m |= tso.debug_dict or {}
+        m |= tso.metrics or {}
+        for key, name in (("global_grad_norm", "global_grad_norm"), ("global_grad_norm_clipped", "global_grad_norm_clipped"),
+                          ("no_overflow_steps", "no_overflow_steps"), ("current_loss_scale", "current_loss_scale")):
+            v = getattr(tso, key)
+            if v is not None:
+                m[f"training/{name}"] = v
+        if tso.overflow is not None:
+            m["training/overflow"] = int(tso.overflow)
+        for g, lr in (tso.learning_rates or {}).items():
+            m[f"training/learning_rate_{g}"] = lr
+        return m
+
+
+def main(launch_config: LaunchConfig, overwrite_config: Optional[dict[str, Any]] = None, return_metrics: bool = False,
+         determined_context: Any = None, determined_profiler: Any = None) -> Optional[list[dict[str, Any]]]:
+    config = _init_transformer_config(launch_config, overwrite_config)
+    topology = Topology(config=config.topology)
+    _init_logger(config, determined_context, topology)
+    if config.training.use_deterministic_torch_algorithms:
+        _enable_deterministic_torch()
+    context = _init_transformer_context(config, determined_context, determined_profiler, launch_config, topology)
+    model = init_model(context=context)
+    optimizer = init_optimizer(context=context, model=model)
+    train_ds: Optional[BaseDataset] = None
+    val_ds: Optional[BaseDataset] = None
+    if topology.is_io_rank:
+        train_ds, val_ds = _read_datasets(context.config)
+    trainer = TransformerTrainer(
+        config=context.config.trainer, context=context, parallel_module=model, optimizer=optimizer, dataset=train_ds,
+        sync_batch_to_model_parallel=_get_sync_batch(context.config.data), loss_function=loss_function,
+        metrics_aggregation_fn=metrics_aggregation_fn, dataset_evaluation=val_ds,
+    )
+    return trainer.run_training(return_metrics=return_metrics)
+
+
+def _get_sync_batch(data_config: DataConfig) -> Callable:
+    if data_config.finetuning_dataset:
+        from .data.finetuning_text_dataset import FinetuningTextDataset
+
+        return FinetuningTextDataset.sync_batch_to_model_parallel
+    if data_config.finetuning_chat_dataset:
+        from .data.finetuning_chat_dataset import FinetuningChatDataset
+
+        return FinetuningChatDataset.sync_batch_to_model_parallel
+    return TextDataset.sync_batch_to_model_parallel
+
+
+def _get_dataset_type(data_config: DataConfig) -> type[BaseBlendedDataset]:
+    if data_config.legacy_dataset:
+        from .data.legacy_blended_dataset import LegacyBlendedDataset
+
+        return LegacyBlendedDataset
+    if data_config.finetuning_dataset:
+        from .data.finetuning_text_dataset import FinetuningTextBlendedDataset
+
+        return FinetuningTextBlendedDataset
+    if data_config.finetuning_chat_dataset:
+        from .data.finetuning_chat_dataset import FinetuningChatBlendedDataset
+
+        return FinetuningChatBlendedDataset
+    return TextBlendedDataset
+
+
+def _read_datasets(config: TransformerConfig) -> tuple[Optional[BaseDataset], Optional[BaseDataset]]:
+    logger.info("loading dataset")
+    datasets, val_datasets = load_datasets(config.data, config.transformer_architecture, config)
+    cls = _get_dataset_type(config.data)
+    seed = config.trainer.seed
+    blended = cls(seed=seed, config=config.data.blended_dataset, datasets=datasets)
+    val = cls(seed=seed, config=config.data.blended_dataset, datasets=val_datasets) if config.data.validation_data_prefixes else None
+    return blended, val
+
+
+def _init_transformer_context(config: TransformerConfig, determined_context: Any, determined_profiler: Any,
+                              launch_config: LaunchConfig, topology: Topology) -> TransformerContext:
+    context = TransformerContext(config=config, topology=topology)
+    if determined_context is not None:
+        context.initialize_with_determined(master_addr=launch_config.master_addr, master_port=str(launch_config.master_port),
+                                           determined_context=determined_context, determined_profiler=determined_profiler,
+                                           seed=config.trainer.seed)
+    else:
+        context.initialize(master_addr=launch_config.master_addr, master_port=str(launch_config.master_port),
+                           seed=config.trainer.seed)
+    return context
+
+
+def _init_logger(config: TransformerConfig, determined_context: Any, topology: Topology) -> None:
+    rank = topology.config.global_rank
+    if config.runner.use_determined:
+        logger.configure_determined(config=config.logger, name=f"RANK {rank}", global_rank=rank,
+                                    determined_context=determined_context)
+    else:
+        logger.configure(config=config.logger, name=f"RANK {rank}", global_rank=rank)
+    logger.log_config(config=config)
+
+
+def _init_transformer_config(launch_config: LaunchConfig, overwrite_config: Optional[dict[str, Any]]) -> TransformerConfig:
+    d = launch_config.payload or overwrite_config or {}
+    d = launch_config.overwrite_config_dict_with_launcher_args(d)
+    return TransformerConfig.from_dict(d, overwrite_values=overwrite_config)
+
+
+def _enable_deterministic_torch() -> None:
+    # the HIP kernels of this package are deterministic by construction (no atomics in reductions);
+    # this pins down the torch/hipBLASLt side
+    os.environ.setdefault("CUBLAS_WORKSPACE_CONFIG", ":4096:8")
+    torch.use_deterministic_algorithms(True)
+
+
+if __name__ == "__main__":
+    main(LaunchConfig.from_launcher_args())
