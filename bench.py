@@ -43,6 +43,9 @@ def _args() -> argparse.Namespace:
     p.add_argument("--sequence-parallel", action="store_true")
     p.add_argument("--zero", type=int, default=1)
     p.add_argument("--num-layers", type=int, default=None, help="debug only: marks the result as not the headline config")
+    p.add_argument("--gemm-tuning", type=str, default="use", choices=["use", "tune", "off"],
+                   help="hipBLASLt solution table (scaling_amd/tuning/gemm_gfx950.csv); tune = benchmark and write")
+    p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
     return p.parse_args()
 
@@ -96,6 +99,9 @@ def main() -> None:
     from scaling_amd.transformer.model import init_model, init_optimizer
     from scaling_amd.transformer.model.model import loss_function, metrics_aggregation_fn
 
+    from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
+
+    gemm_mode = enable_tuned_gemms(a.gemm_tuning, a.gemm_tuning_out, rank)
     arch = llama_architecture(a.model, sequence_length=a.seq_len)
     if a.num_layers is not None:
         arch["num_layers"] = a.num_layers
@@ -177,6 +183,7 @@ def main() -> None:
                 "grad_acc": a.grad_acc,
                 "loss": None if last is None else last.loss,
                 "mfu_palm": None,
+                "gemm_tuning": gemm_mode,
             },
         }
         n_params = sum(p.numel() for p in model.parameters()) * a.tp * a.pp if a.pp == 1 else None

@@ -191,12 +191,27 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 template <typename G>
 __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ x, int64_t n, float scale,
                                                     float* __restrict__ part_sq, float* __restrict__ part_bad) {
+    // x is 16-B aligned here (host peels the unaligned head): 8 elements per thread per trip
     __shared__ float scratch[4];
     float s = 0.f, bad = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = IO<G>::ld(x, i) * scale;
-        if (!isfinite(v)) bad += 1.f;
-        else s += v * v;
+    const int64_t n8 = n / 8, stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+        float v[8];
+        V8<G>::ld(x + 8 * i, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float t = v[j] * scale;
+            const bool fin = isfinite(t);
+            bad += fin ? 0.f : 1.f;
+            s += fin ? t * t : 0.f;
+        }
+    }
+    if (blockIdx.x == 0) {
+        for (int64_t i = 8 * n8 + threadIdx.x; i < n; i += blockDim.x) {
+            const float t = IO<G>::ld(x, i) * scale;
+            if (!isfinite(t)) bad += 1.f;
+            else s += t * t;
+        }
     }
     s = block_sum(s, scratch);
     bad = block_sum(bad, scratch);
@@ -216,6 +231,20 @@ template <typename Src, typename Dst>
 __global__ __launch_bounds__(256) void cast_scale_kernel(const Src* __restrict__ x, Dst* __restrict__ y, int64_t n, float scale) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         IO<Dst>::st(y, i, IO<Src>::ld(x, i) * scale);
+}
+// both pointers 16-B aligned: 8 elements per thread per trip, scalar tail
+template <typename Src, typename Dst>
+__global__ __launch_bounds__(256) void cast_scale_v8_kernel(const Src* __restrict__ x, Dst* __restrict__ y, int64_t n, float scale) {
+    const int64_t n8 = n / 8;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        float v[8];
+        V8<Src>::ld(x + 8 * i, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= scale;
+        V8<Dst>::st(y + 8 * i, v);
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = 8 * n8 + threadIdx.x; i < n; i += blockDim.x) IO<Dst>::st(y, i, IO<Src>::ld(x, i) * scale);
 }
 
 static int gridn(int64_t n, int per = 256, int cap = 4096) {
@@ -268,25 +297,42 @@ void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, 
     }
 #undef SA_ADAM
 }
-int sumsq_blocks(int64_t n) { return gridn(n, 256 * 8, 1024); }
+int sumsq_blocks(int64_t n) { return gridn(n, 256 * 16, 2048) + 1; }
+// bytes of x before its first 16-B boundary, in elements (the scalar head handled by the extra block)
+static int64_t head_elems(const void* x, int esz, int64_t n) {
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(x) & 15;
+    if (mis == 0) return 0;
+    const int64_t h = (int64_t)((16 - mis) / esz);
+    return h < n ? h : n;
+}
 void sumsq(int dtype, const void* x, int64_t n, float scale, float* part_sq, float* part_bad, float* out_sq,
            float* out_bad, int accumulate, hipStream_t st) {
     const int nb = sumsq_blocks(n);
-    if (n > 0) {
-        if (dtype == DT_BF16) hipLaunchKernelGGL(sumsq_kernel<u16>, nb, 256, 0, st, (const u16*)x, n, scale, part_sq, part_bad);
-        else if (dtype == DT_F16) hipLaunchKernelGGL(sumsq_kernel<f16>, nb, 256, 0, st, (const f16*)x, n, scale, part_sq, part_bad);
-        else hipLaunchKernelGGL(sumsq_kernel<float>, nb, 256, 0, st, (const float*)x, n, scale, part_sq, part_bad);
-    } else {
-        hipMemsetAsync(part_sq, 0, sizeof(float) * nb, st);
-        hipMemsetAsync(part_bad, 0, sizeof(float) * nb, st);
-    }
+    const int esz = dtype == DT_F32 ? 4 : 2;
+    const int64_t h = head_elems(x, esz, n);
+    // block nb-1 sums the unaligned head [0, h); blocks [0, nb-1) the aligned rest
+    const char* xb = static_cast<const char*>(x);
+#define SA_SQ(G)                                                                                                       \
+    do {                                                                                                               \
+        hipLaunchKernelGGL(sumsq_kernel<G>, nb - 1, 256, 0, st, (const G*)(xb + h * esz), n - h, scale, part_sq, part_bad); \
+        hipLaunchKernelGGL(sumsq_kernel<G>, 1, 256, 0, st, (const G*)x, h, scale, part_sq + nb - 1, part_bad + nb - 1); \
+    } while (0)
+    if (dtype == DT_BF16) SA_SQ(u16);
+    else if (dtype == DT_F16) SA_SQ(f16);
+    else SA_SQ(float);
+#undef SA_SQ
     hipLaunchKernelGGL(finalize_sum_kernel, 1, 256, 0, st, part_sq, nb, out_sq, accumulate);
     hipLaunchKernelGGL(finalize_sum_kernel, 1, 256, 0, st, part_bad, nb, out_bad, accumulate);
 }
 void cast_scale(int sdt, int ddt, const void* x, void* y, int64_t n, float scale, hipStream_t st) {
     if (n == 0) return;
-    const int g = gridn(n, 256, 8192);
-#define SA_CS(S, D) hipLaunchKernelGGL((cast_scale_kernel<S, D>), g, 256, 0, st, (const S*)x, (D*)y, n, scale)
+    const bool vec = (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (reinterpret_cast<uintptr_t>(y) % 16) == 0;
+    const int g = vec ? gridn(n, 256 * 8, 8192) : gridn(n, 256, 8192);
+#define SA_CS(S, D)                                                                                   \
+    do {                                                                                              \
+        if (vec) hipLaunchKernelGGL((cast_scale_v8_kernel<S, D>), g, 256, 0, st, (const S*)x, (D*)y, n, scale); \
+        else hipLaunchKernelGGL((cast_scale_kernel<S, D>), g, 256, 0, st, (const S*)x, (D*)y, n, scale);        \
+    } while (0)
     if (sdt == DT_BF16) { if (ddt == DT_F32) SA_CS(u16, float); else if (ddt == DT_BF16) SA_CS(u16, u16); else SA_CS(u16, f16); }
     else if (sdt == DT_F16) { if (ddt == DT_F32) SA_CS(f16, float); else if (ddt == DT_BF16) SA_CS(f16, u16); else SA_CS(f16, f16); }
     else { if (ddt == DT_F32) SA_CS(float, float); else if (ddt == DT_BF16) SA_CS(float, u16); else SA_CS(float, f16); }

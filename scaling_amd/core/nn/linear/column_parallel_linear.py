@@ -8,6 +8,7 @@ import torch
 from ...topology import Topology
 from ..parameter_meta import CoreParameterMeta
 from .utils import all_concat, copy_to_tensor_model_parallel_region, get_device
+from .main_grad import linear as main_grad_linear
 
 
 class ColumnParallelLinear(torch.nn.Module):
@@ -56,7 +57,7 @@ class ColumnParallelLinear(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.model_parallel_size > 1 and self.topology is not None and not self.topology.config.sequence_parallel:
             x = copy_to_tensor_model_parallel_region(x, topology=self.topology)
-        out = torch.nn.functional.linear(x, self.weight, self.bias_param)
+        out = main_grad_linear(x, self.weight, self.bias_param)
         if self.parallel_output or self.topology is None:
             return out
         return all_concat(out, dim=-1, topology=self.topology)

@@ -1,0 +1,106 @@
+"""Linear layers whose weight gradient is accumulated by the GEMM itself.
+
+With the framework optimizer every trainable parameter's ``.grad`` is a view into one flat gradient
+buffer (``OptimizerParamGroup.attach_grads`` tags such parameters with ``_sa_main_grad``).  For those
+weights the backward issues ``grad.addmm_(dY^T, X)`` — hipBLASLt's beta=1 epilogue — instead of
+materialising ``dW`` and letting autograd add it into ``.grad``: one GEMM, no extra ``[N, K]``
+temporary, no elementwise accumulate pass, and a single bf16 rounding of ``grad + dY^T X``.
+The optimizer's bucket-ready callback (``_sa_grad_ready``) is invoked in place of autograd's
+post-accumulate-grad hook.
+
+Several weights that read the same input (q/k/v, SwiGLU ``dense_in``/``siglu_weight``) run as ONE
+GEMM.  When the weights (and their gradients) sit back to back in the flat buffers the combined
+``[sum N, K]`` matrix is a zero-copy strided view; otherwise it is concatenated.
+"""
+from __future__ import annotations
+
+from typing import Any, Optional, Sequence
+
+import torch
+
+
+def _adjacent(ts: Sequence[Optional[torch.Tensor]]) -> Optional[torch.Tensor]:
+    """Zero-copy [sum N, K] view over row-major tensors stored back to back, else None."""
+    if any(t is None for t in ts):
+        return None
+    first = ts[0]
+    assert first is not None
+    if len(ts) == 1:
+        return first if first.is_contiguous() else None
+    K = first.shape[-1]
+    es = first.element_size()
+    nxt = first.data_ptr()
+    for t in ts:
+        assert t is not None
+        if not t.is_contiguous() or t.shape[-1] != K or t.dtype != first.dtype or t.data_ptr() != nxt:
+            return None
+        if t.untyped_storage().data_ptr() != first.untyped_storage().data_ptr():
+            return None
+        nxt += t.numel() * es
+    rows = sum(t.shape[0] for t in ts)  # type: ignore[union-attr]
+    return torch.as_strided(first, (rows, K), (K, 1))
+
+
+def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
+    if not all(getattr(w, "_sa_main_grad", False) and w.grad is not None for w in weights):
+        return None
+    return _adjacent([w.grad for w in weights])
+
+
+class _MultiLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx: Any, x: torch.Tensor, n: int, *params: Optional[torch.Tensor]) -> torch.Tensor:  # type: ignore[override]
+        weights = params[:n]
+        biases = params[n:]
+        w = _adjacent(weights)
+        if w is None:
+            w = torch.cat(weights, dim=0)  # type: ignore[arg-type]
+        has_bias = len(biases) > 0 and biases[0] is not None
+        b = None
+        if has_bias:
+            b = biases[0] if n == 1 else torch.cat(biases, dim=0)  # type: ignore[arg-type]
+        out = torch.nn.functional.linear(x, w, b)
+        ctx.save_for_backward(x, w, *weights)
+        ctx.n, ctx.has_bias = n, has_bias
+        ctx.splits = [t.shape[0] for t in weights]  # type: ignore[union-attr]
+        return out
+
+    @staticmethod
+    def backward(ctx: Any, g: torch.Tensor):  # type: ignore[override]
+        x, w, *weights = ctx.saved_tensors
+        n = ctx.n
+        dx = torch.matmul(g, w) if ctx.needs_input_grad[0] else None
+        dws: list[Optional[torch.Tensor]] = [None] * n
+        if any(ctx.needs_input_grad[2 : 2 + n]):
+            g2 = g.reshape(-1, g.shape[-1])
+            x2 = x.reshape(-1, x.shape[-1])
+            target = _main_grad_target(weights)
+            if target is not None:
+                target.addmm_(g2.t(), x2)
+                for wt in weights:
+                    cb = getattr(wt, "_sa_grad_ready", None)
+                    if cb is not None:
+                        cb(wt)
+            else:
+                dw = torch.matmul(g2.t(), x2)
+                dws = list(torch.split(dw, ctx.splits, dim=0)) if n > 1 else [dw]
+        dbs: list[Optional[torch.Tensor]] = []
+        if ctx.has_bias:
+            gb = g.reshape(-1, g.shape[-1]).sum(0)
+            dbs = list(torch.split(gb, ctx.splits, dim=0)) if n > 1 else [gb]
+        return (dx, None, *dws, *dbs)
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear`` with GEMM-fused gradient accumulation for main-grad weights."""
+    if bias is None:
+        return _MultiLinear.apply(x, 1, weight)
+    return _MultiLinear.apply(x, 1, weight, bias)
+
+
+def multi_linear(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Optional[Sequence[Optional[torch.Tensor]]] = None
+                 ) -> torch.Tensor:
+    """``x @ [W_1; ...; W_n]^T (+ [b_1; ...; b_n])`` as one GEMM (forward, dgrad and wgrad)."""
+    if biases is None or any(b is None for b in biases):
+        return _MultiLinear.apply(x, len(weights), *weights)
+    return _MultiLinear.apply(x, len(weights), *weights, *biases)

@@ -11,6 +11,7 @@ import torch
 from ...topology import Topology
 from ..parameter_meta import CoreParameterMeta
 from .utils import all_reduce, all_shard, get_device
+from .main_grad import linear as main_grad_linear
 
 
 class RowParallelLinear(torch.nn.Module):
@@ -61,7 +62,7 @@ class RowParallelLinear(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not self.parallel_input and self.topology is not None:
             x = all_shard(x, dim=-1, topology=self.topology)
-        out = torch.nn.functional.linear(x, self.weight)
+        out = main_grad_linear(x, self.weight)
         if not self.parallel_output and self.topology is not None:
             out = all_reduce(out, topology=self.topology)
         b = self.bias_param

@@ -67,7 +67,9 @@ class Optimizer(BaseOptimizer):
             for gi, g in enumerate(parameter_groups):
                 for pi, p in enumerate(g.parameters_original):
                     if p.requires_grad and hasattr(p, "register_post_accumulate_grad_hook"):
-                        self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(gi, pi)))
+                        hook = self._make_hook(gi, pi)
+                        self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                        p._sa_grad_ready = hook  # type: ignore[attr-defined]  # GEMM-accumulated grads
 
     # ------------------------------------------------------------------ bookkeeping
     def _assert_no_parameter_duplicates(self) -> None:

@@ -114,6 +114,7 @@ class OptimizerParamGroup:
             g = self.flat_grad[o : o + n].view_as(p)
             if p.grad is None or p.grad.data_ptr() != g.data_ptr():
                 p.grad = g
+            p._sa_main_grad = True  # type: ignore[attr-defined]  # linear layers may addmm_ into .grad
 
     def owned_ranges(self, param_index: int) -> list[tuple[int, int, int]]:
         """(owned_start, param_local_start, length) pieces of parameter `param_index` owned by this rank."""

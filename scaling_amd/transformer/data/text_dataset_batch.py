@@ -84,6 +84,13 @@ class TextDatasetBatch(BaseDatasetBatch):
             if self.loss_weights is None:
                 self.loss_weights = torch.ones_like(input_token_ids, dtype=torch.float).contiguous()
 
+    def contiguous_(self) -> "TextDatasetBatch":
+        for n in self._FIELDS:
+            v = getattr(self, n)
+            if isinstance(v, torch.Tensor):
+                setattr(self, n, v.contiguous())
+        return self
+
     def only_inputs(self) -> "TextDatasetBatch":
         return TextDatasetBatch(input_token_ids=self.input_token_ids, input_images=self.input_images,
                                 input_image_locations=self.input_image_locations, position_ids=self.position_ids,

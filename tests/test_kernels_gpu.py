@@ -167,6 +167,25 @@ def test_sumsq():
     assert out[1].item() == 1
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("offset", [0, 1, 3, 7, 8])
+def test_sumsq_cast_unaligned(dtype, offset):
+    # views at element offsets that are not 16-B aligned exercise the scalar head / vector body split
+    base = torch.randn(1_000_003 + offset, device=DEV, dtype=dtype)
+    x = base[offset:]
+    out = torch.zeros(2, device=DEV)
+    optim.sumsq_nonfinite_(x, out, scale=2.0, accumulate=False)
+    ref = ((x.double() * 2.0) ** 2).sum().float()
+    torch.testing.assert_close(out[0], ref, rtol=1e-4, atol=1e-2)
+    x[offset + 11] = float("nan")
+    x[-1] = float("inf")
+    optim.sumsq_nonfinite_(x, out, accumulate=False)
+    assert out[1].item() == 2
+    y = torch.empty(x.numel() + 3, device=DEV, dtype=torch.float32)[3:]
+    optim.cast_scale_(x, y, 0.5)
+    torch.testing.assert_close(y, x.float() * 0.5, equal_nan=True)
+
+
 def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0):
     torch.manual_seed(seed)
     T = sum(lens)
