@@ -265,9 +265,10 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
     auto dk = at::empty({Tk, Hk, D}, k.options());
     auto dv = at::empty({Tk, Hk, D}, v.options());
     auto delta = at::empty({H, T}, q.options().dtype(at::kFloat));
+    auto lse2 = at::empty({H, T}, q.options().dtype(at::kFloat));
     BwdArgs a{};
     a.q = (const uint16_t*)q.data_ptr(); a.k = (const uint16_t*)k.data_ptr(); a.v = (const uint16_t*)v.data_ptr();
-    a.dO = (const uint16_t*)dO.data_ptr(); a.lse = lse.data_ptr<float>(); a.delta = delta.data_ptr<float>();
+    a.dO = (const uint16_t*)dO.data_ptr(); a.lse = lse.data_ptr<float>(); a.delta = delta.data_ptr<float>(); a.lse2 = lse2.data_ptr<float>();
     a.dq = (uint16_t*)dq.data_ptr(); a.dk = (uint16_t*)dk.data_ptr(); a.dv = (uint16_t*)dv.data_ptr();
     a.q_tok = q.stride(0); a.q_head = q.stride(1); a.k_tok = k.stride(0); a.k_head = k.stride(1);
     a.v_tok = v.stride(0); a.v_head = v.stride(1); a.do_tok = dO.stride(0); a.do_head = dO.stride(1);

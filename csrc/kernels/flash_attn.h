@@ -53,10 +53,7 @@ __device__ __forceinline__ bf16x8 ld_tr(const char* lds, int kb, int c0) {
     const int col = c0 + 16 * g + 4 * (i & 3);
     s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lds_off<D>(row, col)));
     s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds + lds_off<D>(row + 8, col)));
-    s16x4 c = {a[0], a[1], a[2], a[3]};
-    typedef short s16x8v __attribute__((ext_vector_type(8)));
-    s16x8v r = {c[0], c[1], c[2], c[3], b[0], b[1], b[2], b[3]};
-    return __builtin_bit_cast(bf16x8, r);
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // pack accumulator registers 8s..8s+7 into a bf16 B-operand fragment
@@ -92,6 +89,79 @@ struct Stage {
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// dword 3 of a raw buffer resource on gfx9/CDNA (32-bit data format, no swizzle); out-of-range
+// loads return 0
+constexpr int kBufFlags = 0x00020000;
+
+// buffer resource from values the compiler cannot prove wave-uniform (they are): readfirstlane
+// keeps the descriptor in SGPRs instead of a per-load waterfall loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t nbytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const uint64_t u = ((uint64_t)hi << 32) | lo;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0, __builtin_amdgcn_readfirstlane(nbytes),
+                                             kBufFlags);
+}
+
+// LDS-DMA of a 64-row x D bf16 tile into its swizzled LDS image by the W waves of a workgroup:
+// buffer_load_dwordx4 ... lds writes 64 lanes x 16 B = 1 KiB linearly at M0, so each lane reads the
+// global chunk that belongs at its linear LDS position (source-permuted swizzle).  Rows past the
+// resource range land as zeros.  No staging registers, no ds_write; completion is the vmcnt(0)
+// the compiler places before the next __syncthreads().
+typedef __attribute__((address_space(3))) void lds_void;
+template <int D, int W>
+struct DmaTile {
+    static constexpr int PIECES = 64 * D * 2 / 1024;
+    static constexpr int NPW = PIECES / W;
+    static_assert(NPW >= 1 && NPW * W == PIECES, "tile pieces must split evenly across waves");
+    int voff[NPW];
+    __device__ __forceinline__ void init(int wave, int lane, int64_t tok) {
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) {
+            const int p = (wave + W * i) * 1024 + lane * 16;
+            const int row = p / (2 * D), slot = (p % (2 * D)) / 16;
+            voff[i] = row * (int)tok * 2 + 16 * (slot ^ swz<D>(row, 0));
+        }
+    }
+    __device__ __forceinline__ void load(const void* base, int64_t tok, int rows, char* tile, int wave_u) const {
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(base, (uint32_t)max(rows, 0) * (uint32_t)tok * 2u);
+#pragma unroll
+        for (int i = 0; i < NPW; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(tile + (wave_u + W * i) * 1024), 16, voff[i], 0, 0, 0);
+    }
+};
+
+template <int D, int W>
+__device__ __forceinline__ void dma_load(const DmaTile<D, W>& t, const void* base, int64_t tok, int rows, char* tile,
+                                         int wave_u) {
+    t.load(base, tok, rows, tile, wave_u);
+}
+
+// 3-way max without the canonicalising v_max the compiler wraps around fmaxf
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// lane l and lane l^32 combined with one v_permlane32_swap: returns {x_l, x_(l^32)} in some order
+__device__ __forceinline__ void xchg32(float x, float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_xchg32(float x) {
+    float a, b;
+    xchg32(x, a, b);
+    return vmax3(a, b, a);
+}
+__device__ __forceinline__ float sum_xchg32(float x) {
+    float a, b;
+    xchg32(x, a, b);
+    return a + b;
+}
+// row offset (r) of accumulator register j in a 32x32 MFMA C tile, excluding the 4h lane term
+__host__ __device__ constexpr int crow(int j) { return (j & 3) + 8 * (j >> 2); }
 
 }  // namespace fa
 }  // namespace sa

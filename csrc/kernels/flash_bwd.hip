@@ -17,7 +17,8 @@ using namespace sa::fa;
 template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const u16* __restrict__ o, int64_t o_tok, int64_t o_head,
                                                          const u16* __restrict__ dO, int64_t d_tok, int64_t d_head,
-                                                         float* __restrict__ delta, int64_t T, int H) {
+                                                         float* __restrict__ delta, const float* __restrict__ lse,
+                                                         float* __restrict__ lse2, int64_t T, int H) {
     constexpr int LPR = D / 8;  // lanes per row
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t row = gid / LPR;
@@ -37,31 +38,64 @@ __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const u16* __restrict__
     }
 #pragma unroll
     for (int w = LPR / 2; w > 0; w >>= 1) s += __shfl_xor(s, w, 64);
-    if (ok && c == 0) delta[(int64_t)hh * T + t] = s;
+    if (ok && c == 0) {
+        delta[(int64_t)hh * T + t] = s;
+        lse2[(int64_t)hh * T + t] = lse[(int64_t)hh * T + t] * 1.4426950408889634f;
+    }
 }
 
+// Shared by both kernels: per-lane LDS offsets of row fragments (row lk, cols 16ks + 8h) and of
+// transposed fragments (rows 4h + i/4 (+8), cols 32t + 16g + 4(i&3)); tile bases and the 32/16-row
+// block offsets are compile-time immediates (loops unrolled per buffer).
 template <int D>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(BwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int TILE = 64 * D * 2;
-    // layout: K image [128][D] | V image [128][D] | 2 x (Q tile | dO tile) | 2 x (lse[64] | delta[64])
-    char* kimg = smem;
-    char* vimg = smem + 2 * TILE;
-    char* qbuf = smem + 4 * TILE;  // buffer b: Q at qbuf + 2*b*TILE, dO at +TILE
-    float* stat = reinterpret_cast<float*>(smem + 8 * TILE);  // buffer b: lse at stat + 128*b, delta +64
+struct LdsOffsets {
+    int row[D / 16];
+    int tr[D / 32][2];
+    __device__ __forceinline__ void init(int lane) {
+        const int h = lane >> 5, r = lane & 31, g = (lane >> 4) & 1, i = lane & 15;
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) row[ks] = lds_off<D>(r, 16 * ks + 8 * h);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+            tr[t][0] = lds_off<D>(4 * h + (i >> 2), 32 * t + 16 * g + 4 * (i & 3));
+            tr[t][1] = lds_off<D>(4 * h + (i >> 2) + 8, 32 * t + 16 * g + 4 * (i & 3));
+        }
+    }
+};
+template <int D>
+__device__ __forceinline__ bf16x8 rd_row(const char* tile, int imm, int off) {
+    return *reinterpret_cast<const bf16x8*>(tile + imm + off);
+}
+template <int D>
+__device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const int (&tr)[2]) {
+    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + tr[0]));
+    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + tr[1]));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 
-    const int seg = blockIdx.z, hk = blockIdx.y;
+// dK / dV: workgroup = 4 waves x 32 keys of one (segment, kv head); the key is on the MFMA lane: each
+// wave reads its K and V rows (B operands) from the workgroup's K/V image for the whole sweep over the
+// GQA group's q heads x 64-query tiles.  Q, dO, lse2 (= lse * log2 e) and delta arrive by LDS-DMA
+// into a double buffer (no staging registers), so the 256-register cap holds S / dP in arch VGPRs
+// and dK / dV never bounce through v_accvgpr moves.  Per 32-query block:
+//   S = Q K^T, dP = dO V^T (row reads), p = exp2(S c - lse2), dS = p (dP - delta),
+//   dV^T += dO^T P, dK^T += Q^T dS (transposed reads; P / dS accumulators are the B operands).
+// Query rows past the segment arrive as zeros (Q = dO = 0, lse2 = delta = 0) and contribute nothing.
+template <int D>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int TILE = 64 * D * 2, BUF = 2 * TILE + 512, NKS = D / 16, NT = D / 32;
+    // grid (Hkv, nseg, key blocks): key block slowest so causal work is issued heaviest-first
+    const int seg = blockIdx.y, hk = blockIdx.x;
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
-    const int kwg0 = blockIdx.x * 128;
+    const int kwg0 = blockIdx.z * 128;
     if (kwg0 >= Lk) return;
     const int grp = a.Hq / a.Hkv;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, lk = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, lk = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int off = Lk - Lq;
-    const int mykey_rel = wave * 32 + lk;  // row in K/V image
-    const int mykey = kwg0 + mykey_rel;
-
-    // query range touching these keys
+    const int kw0 = kwg0 + 32 * wave, mykey = kw0 + lk;
     const int klast = min(kwg0 + 127, Lk - 1);
     int qlo = 0, qhi = Lq;
     if (a.causal) qlo = max(0, kwg0 - off);
@@ -73,76 +107,71 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(BwdArgs a) {
     const int ntq = qhi > qlo ? (qhi - qlo + 63) / 64 : 0;
     const int nwork = ntq * grp;
 
-    {  // K/V images for the workgroup's 128 keys
-        Stage<D> st;
+    char* kimg = smem + 2 * BUF;  // K rows [0, 128) then V rows [0, 128)
+    {
+        DmaTile<D, 4> dk_, dv_;
+        dk_.init(wave, lane, a.k_tok);
+        dv_.init(wave, lane, a.v_tok);
         const u16* kb = a.k + (int64_t)(k0s + kwg0) * a.k_tok + (int64_t)hk * a.k_head;
         const u16* vb = a.v + (int64_t)(k0s + kwg0) * a.v_tok + (int64_t)hk * a.v_head;
-        st.load(kb, a.k_tok, min(64, Lk - kwg0));
-        st.store(kimg);
-        st.load(kb + 64 * a.k_tok, a.k_tok, max(0, min(64, Lk - kwg0 - 64)));
-        st.store(kimg + TILE);
-        st.load(vb, a.v_tok, min(64, Lk - kwg0));
-        st.store(vimg);
-        st.load(vb + 64 * a.v_tok, a.v_tok, max(0, min(64, Lk - kwg0 - 64)));
-        st.store(vimg + TILE);
+        dk_.load(kb, a.k_tok, Lk - kwg0, kimg, wave);
+        dk_.load(kb + 64 * a.k_tok, a.k_tok, Lk - kwg0 - 64, kimg + TILE, wave);
+        dv_.load(vb, a.v_tok, Lk - kwg0, kimg + 2 * TILE, wave);
+        dv_.load(vb + 64 * a.v_tok, a.v_tok, Lk - kwg0 - 64, kimg + 3 * TILE, wave);
     }
-    f32x16 dk[D / 32], dv[D / 32];
+    const char* kw_img = kimg + 32 * wave * D * 2;
+    const char* vw_img = kimg + 2 * TILE + 32 * wave * D * 2;
+    LdsOffsets<D> lo;
+    lo.init(lane);
+    DmaTile<D, 4> tq, td;
+    tq.init(wave, lane, a.q_tok);
+    td.init(wave, lane, a.do_tok);
+    auto issue = [&](int w, char* buf) {
+        const int gi = w / ntq, qt = qlo + (w % ntq) * 64, hq = hk * grp + gi;
+        tq.load(a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
+        td.load(a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
+        if (wave == 0) {  // 64 lse2 then 64 delta: one dword per lane each
+            const int64_t ix = (int64_t)hq * a.lse_stride + q0s + qt;
+            const uint32_t nb = (uint32_t)max(min(64, Lq - qt), 0) * 4u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
+        }
+    };
+    f32x16 dk[NT], dv[NT];
 #pragma unroll
-    for (int t = 0; t < D / 32; ++t) { dk[t] = f32x16{}; dv[t] = f32x16{}; }
+    for (int t = 0; t < NT; ++t) { dk[t] = f32x16{}; dv[t] = f32x16{}; }
+    const float c2 = a.scale_log2;
 
-    Stage<D> sq, sd;
-    float st_l = 0.f, st_d = 0.f;
-    auto issue = [&](int w) {
-        const int gi = w / ntq, qt = qlo + (w % ntq) * 64;
-        const int hq = hk * grp + gi;
-        const int valid = min(64, Lq - qt);
-        sq.load(a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, valid);
-        sd.load(a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, valid);
-        if (threadIdx.x < 64) {
-            const int r = threadIdx.x;
-            const bool ok = r < valid;
-            st_l = ok ? a.lse[(int64_t)hq * a.lse_stride + q0s + qt + r] * 1.4426950408889634f : INFINITY;
-            st_d = ok ? a.delta[(int64_t)hq * a.lse_stride + q0s + qt + r] : 0.f;
-        }
-    };
-    auto commit = [&](int b) {
-        sq.store(qbuf + 2 * b * TILE);
-        sd.store(qbuf + (2 * b + 1) * TILE);
-        if (threadIdx.x < 64) {
-            stat[128 * b + threadIdx.x] = st_l;
-            stat[128 * b + 64 + threadIdx.x] = st_d;
-        }
-    };
-    if (nwork > 0) {
-        issue(0);
-        commit(0);
-    }
-    __syncthreads();
-    int cur = 0;
-    for (int w = 0; w < nwork; ++w) {
-        const bool has_next = w + 1 < nwork;
-        if (has_next) issue(w + 1);
-        const int qt = qlo + (w % ntq) * 64;
-        const char* Q = qbuf + 2 * cur * TILE;
+    auto tile = [&](const char* Q, int w) {
         const char* DO = Q + TILE;
-        const float* LS = stat + 128 * cur;
+        const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
         const float* DL = LS + 64;
-        // ---- S = Q K^T, dP = dO V^T  (2 query blocks of 32)
-        f32x16 s[2] = {f32x16{}, f32x16{}}, dp[2] = {f32x16{}, f32x16{}};
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-            const bf16x8 kf = ld_row<D>(kimg, mykey_rel, 16 * ks + 8 * h);
-            const bf16x8 vf = ld_row<D>(vimg, mykey_rel, 16 * ks + 8 * h);
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                s[b] = mfma(ld_row<D>(Q, 32 * b + lk, 16 * ks + 8 * h), kf, s[b]);
-                dp[b] = mfma(ld_row<D>(DO, 32 * b + lk, 16 * ks + 8 * h), vf, dp[b]);
-            }
-        }
-        const bool need_mask = (kwg0 + 128 > Lk) || (qt + 64 > Lq) || (a.causal && qt < kwg0 + 127 - off) ||
-                               (a.window >= 0);
+        const int qt = qlo + (w % ntq) * 64;
+        const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
+                               (a.window >= 0 && (kw0 < qt + 63 + off - a.window || (!a.causal && kw0 + 31 > qt + off + a.window)));
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
+            f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                s = mfma(rd_row<D>(Q, 32 * b * D * 2, lo.row[ks]), rd_row<D>(kw_img, 0, lo.row[ks]), s);
+                dp = mfma(rd_row<D>(DO, 32 * b * D * 2, lo.row[ks]), rd_row<D>(vw_img, 0, lo.row[ks]), dp);
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            // query of register j: qt + 32b + 4h + crow(j)
+            int mlo = -1 << 30, mhi = 1 << 30;
+            if (need_mask) {
+                const int rel = mykey - off - qt - 32 * b - 4 * h;
+                if (a.causal) mlo = rel;                  // key <= q + off
+                if (a.window >= 0) {
+                    mhi = rel + a.window;                 // key >= q + off - window
+                    if (!a.causal) mlo = rel - a.window;  // key <= q + off + window
+                }
+            }
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 32 * b + 8 * g + 4 * h);
@@ -150,41 +179,50 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int r = 4 * g + j;
-                    float p = fast_exp2(s[b][r] * a.scale_log2 - l4[j]);
-                    if (need_mask) {
-                        const int q = qt + 32 * b + 8 * g + 4 * h + j;
-                        bool ok = mykey < Lk && q < Lq;
-                        if (a.causal) ok = ok && mykey <= q + off;
-                        if (a.window >= 0) ok = ok && mykey >= q + off - a.window && (a.causal || mykey <= q + off + a.window);
-                        p = ok ? p : 0.f;
-                    }
-                    s[b][r] = p;
-                    dp[b][r] = p * (dp[b][r] - d4[j]);
+                    float p = fast_exp2(__builtin_fmaf(s[r], c2, -l4[j]));
+                    if (need_mask) p = (crow(r) >= mlo && crow(r) <= mhi) ? p : 0.f;
+                    s[r] = p;
+                    dp[r] = p * (dp[r] - d4[j]);
                 }
             }
-        }
-        // ---- dV^T += dO^T P ; dK^T += Q^T dS
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 pb = pack_acc(s[b], ss);
-                const bf16x8 db = pack_acc(dp[b], ss);
+                const bf16x8 pb = pack_acc(s, ss), db = pack_acc(dp, ss);
+                const int kb = (32 * b + 16 * ss) * D * 2;
 #pragma unroll
-                for (int t = 0; t < D / 32; ++t) {
-                    dv[t] = mfma(ld_tr<D>(DO, 32 * b + 16 * ss, 32 * t), pb, dv[t]);
-                    dk[t] = mfma(ld_tr<D>(Q, 32 * b + 16 * ss, 32 * t), db, dk[t]);
+                for (int t = 0; t < NT; ++t) {
+                    dv[t] = mfma(rd_tr<D>(DO, kb, lo.tr[t]), pb, dv[t]);
+                    dk[t] = mfma(rd_tr<D>(Q, kb, lo.tr[t]), db, dk[t]);
                 }
             }
-        if (has_next) commit(cur ^ 1);
+#pragma unroll
+            for (int i = 0; i < 4 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            }
+        }
+    };
+
+    char* buf0 = smem;
+    char* buf1 = smem + BUF;
+    if (nwork > 0) issue(0, buf0);
+    __syncthreads();
+    int w = 0;
+    for (; w + 1 < nwork; w += 2) {
+        issue(w + 1, buf1);
+        tile(buf0, w);
         __syncthreads();
-        cur ^= 1;
+        if (w + 2 < nwork) issue(w + 2, buf0);
+        tile(buf1, w + 1);
+        __syncthreads();
     }
+    if (w < nwork) tile(buf0, w);
+
     if (mykey < Lk) {
         u16* kp = a.dk + (int64_t)(k0s + mykey) * a.dk_tok + (int64_t)hk * a.dk_head;
         u16* vp = a.dv + (int64_t)(k0s + mykey) * a.dv_tok + (int64_t)hk * a.dv_head;
 #pragma unroll
-        for (int t = 0; t < D / 32; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 u16x4 wk, wv;
@@ -199,18 +237,22 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(BwdArgs a) {
     }
 }
 
+// dQ: workgroup = 4 waves x 32 queries of one (segment, q head); query on the lane (Q, dO rows are
+// register-resident B operands), K / V tiles of 64 keys double-buffered in LDS by LDS-DMA.  Per 32-key block:
+//   S^T = K Q^T, dP^T = V dO^T, p = exp2(S c - lse2), dS = p (dP - delta), dQ^T += K^T dS^T.
 template <int D>
-__global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(BwdArgs a) {
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int TILE = 64 * D * 2;
-    const int seg = blockIdx.z, hq = blockIdx.y;
+    constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
+    const int seg = blockIdx.y, hq = blockIdx.x;  // grid (Hq, nseg, q tiles), heaviest tiles first
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int ntiles_q = (Lq + 127) / 128;
-    const int qt = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+    const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, lq = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     const int off = Lk - Lq;
     const int qwg0 = qt * 128, qw0 = qwg0 + wave * 32, myq = qw0 + lq;
     const int qlast = min(qwg0 + 127, Lq - 1);
@@ -221,84 +263,95 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dq_kernel(BwdArgs a) {
     if (a.window >= 0) klo = max(0, qwg0 + off - a.window);
     klo = (klo / 64) * 64;
 
-    bf16x8 qf[D / 16], df[D / 16];
-    const int qrow = q0s + min(myq, Lq - 1);
+    bf16x8 qf[NKS], df[NKS];
     {
+        const int qrow = q0s + min(myq, Lq - 1);
         const u16* qp = a.q + (int64_t)qrow * a.q_tok + (int64_t)hq * a.q_head;
         const u16* dp = a.dO + (int64_t)qrow * a.do_tok + (int64_t)hq * a.do_head;
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
+        for (int ks = 0; ks < NKS; ++ks) {
             qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * h));
             df[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(dp + 16 * ks + 8 * h));
         }
     }
-    const float lse2 = myq < Lq ? a.lse[(int64_t)hq * a.lse_stride + q0s + myq] * 1.4426950408889634f : INFINITY;
+    const float nl2 = myq < Lq ? -a.lse[(int64_t)hq * a.lse_stride + q0s + myq] * 1.4426950408889634f : -INFINITY;
     const float dlt = myq < Lq ? a.delta[(int64_t)hq * a.lse_stride + q0s + myq] : 0.f;
-    f32x16 dq[D / 32];
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) dq[t] = f32x16{};
-
+    LdsOffsets<D> lo;
+    lo.init(lane);
+    DmaTile<D, 4> tk, tv;
+    tk.init(wave_u, lane, a.k_tok);
+    tv.init(wave_u, lane, a.v_tok);
     const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
-    Stage<D> sk, sv;
-    int cur = 0;
-    if (klo < khi) {
-        sk.load(kbase + (int64_t)klo * a.k_tok, a.k_tok, min(64, Lk - klo));
-        sv.load(vbase + (int64_t)klo * a.v_tok, a.v_tok, min(64, Lk - klo));
-        sk.store(smem);
-        sv.store(smem + TILE);
-    }
-    __syncthreads();
-    for (int kt = klo; kt < khi; kt += 64) {
-        const bool has_next = kt + 64 < khi;
-        if (has_next) {
-            sk.load(kbase + (int64_t)(kt + 64) * a.k_tok, a.k_tok, min(64, Lk - kt - 64));
-            sv.load(vbase + (int64_t)(kt + 64) * a.v_tok, a.v_tok, min(64, Lk - kt - 64));
-        }
-        const char* K = smem + 2 * cur * TILE;
+    // (DMA issued through the free function dma_load: a direct DmaTile::load call in this kernel makes
+    //  hipcc's host pass treat the kernel as undefined and drop its launch stub)
+#define SA_DQ_ISSUE(KT, BUFP)                                                                 \
+    do {                                                                                      \
+        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);        \
+        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u); \
+    } while (0)
+    f32x16 dq[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) dq[t] = f32x16{};
+    const float c2 = a.scale_log2;
+
+    auto tile = [&](const char* K, int kt) {
         const char* V = K + TILE;
-        f32x16 s[2] = {f32x16{}, f32x16{}}, dp[2] = {f32x16{}, f32x16{}};
+        const bool need_mask = (kt + 64 > Lk) || (a.causal && kt + 63 > qw0 + off) ||
+                               (a.window >= 0 && (kt < qw0 + 31 + off - a.window || (!a.causal && kt + 63 > qw0 + off + a.window)));
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks)
+        for (int b = 0; b < 2; ++b) {
+            f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                s[b] = mfma(ld_row<D>(K, 32 * b + lq, 16 * ks + 8 * h), qf[ks], s[b]);
-                dp[b] = mfma(ld_row<D>(V, 32 * b + lq, 16 * ks + 8 * h), df[ks], dp[b]);
+            for (int ks = 0; ks < NKS; ++ks) {
+                s = mfma(rd_row<D>(K, 32 * b * D * 2, lo.row[ks]), qf[ks], s);
+                dp = mfma(rd_row<D>(V, 32 * b * D * 2, lo.row[ks]), df[ks], dp);
             }
-        const bool need_mask = (kt + 64 > Lk) || (a.causal && kt + 63 > qw0 + off) || (a.window >= 0);
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
+            // key of register j: kt + 32b + 4h + crow(j)
+            int hi = 1 << 30, low = -1 << 30;
+            if (need_mask) {
+                const int base = kt + 32 * b + 4 * h;
+                hi = Lk - 1 - base;
+                if (a.causal) hi = min(hi, myq + off - base);
+                else if (a.window >= 0) hi = min(hi, myq + off + a.window - base);
+                if (a.window >= 0) low = myq + off - a.window - base;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                float p = fast_exp2(s[b][r] * a.scale_log2 - lse2);
-                if (need_mask) {
-                    const int key = kt + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    bool ok = key < Lk && myq < Lq;
-                    if (a.causal) ok = ok && key <= myq + off;
-                    if (a.window >= 0) ok = ok && key >= myq + off - a.window && (a.causal || key <= myq + off + a.window);
-                    p = ok ? p : 0.f;
-                }
-                dp[b][r] = p * (dp[b][r] - dlt);
+                float p = fast_exp2(__builtin_fmaf(s[r], c2, nl2));
+                if (need_mask) p = (crow(r) <= hi && crow(r) >= low) ? p : 0.f;
+                dp[r] = p * (dp[r] - dlt);
             }
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 db = pack_acc(dp[b], ss);
+                const bf16x8 db = pack_acc(dp, ss);
+                const int kb = (32 * b + 16 * ss) * D * 2;
 #pragma unroll
-                for (int t = 0; t < D / 32; ++t) dq[t] = mfma(ld_tr<D>(K, 32 * b + 16 * ss, 32 * t), db, dq[t]);
+                for (int t = 0; t < NT; ++t) dq[t] = mfma(rd_tr<D>(K, kb, lo.tr[t]), db, dq[t]);
             }
-        if (has_next) {
-            sk.store(smem + 2 * (cur ^ 1) * TILE);
-            sv.store(smem + (2 * (cur ^ 1) + 1) * TILE);
         }
+    };
+
+    char* buf0 = smem;
+    char* buf1 = smem + 2 * TILE;
+    if (klo < khi) SA_DQ_ISSUE(klo, buf0);
+    __syncthreads();
+    const int ntiles = khi > klo ? (khi - klo + 63) / 64 : 0;
+    int kt = klo;
+    for (int pr = 0; pr < ntiles / 2; ++pr, kt += 128) {
+        SA_DQ_ISSUE(kt + 64, buf1);
+        tile(buf0, kt);
         __syncthreads();
-        cur ^= 1;
+        if (kt + 128 < khi) SA_DQ_ISSUE(kt + 128, buf0);
+        tile(buf1, kt + 64);
+        __syncthreads();
     }
+    if (ntiles & 1) tile(buf0, kt);
+#undef SA_DQ_ISSUE
     if (myq < Lq) {
         u16* qp = a.dq + (int64_t)(q0s + myq) * a.dq_tok + (int64_t)hq * a.dq_head;
 #pragma unroll
-        for (int t = 0; t < D / 32; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 u16x4 w;
@@ -315,19 +368,19 @@ void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, 
     {
         const int64_t threads = Tq * a.Hq * (D / 8);
         const int grid = (int)((threads + 255) / 256);
-        if (D == 128) hipLaunchKernelGGL(fa_bwd_dot_kernel<128>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, Tq, a.Hq);
-        else if (D == 64) hipLaunchKernelGGL(fa_bwd_dot_kernel<64>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, Tq, a.Hq);
-        else hipLaunchKernelGGL(fa_bwd_dot_kernel<32>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, Tq, a.Hq);
+        if (D == 128) hipLaunchKernelGGL(fa_bwd_dot_kernel<128>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
+        else if (D == 64) hipLaunchKernelGGL(fa_bwd_dot_kernel<64>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
+        else hipLaunchKernelGGL(fa_bwd_dot_kernel<32>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
     }
     {
-        dim3 grid((max_k + 127) / 128, a.Hkv, a.nseg);
-        const size_t lds = 8 * 64 * D * 2 + 2 * 128 * sizeof(float);
+        dim3 grid(a.Hkv, a.nseg, (max_k + 127) / 128);
+        const size_t lds = 2 * (2 * 64 * D * 2 + 512) + 4 * 64 * D * 2;
         if (D == 128) hipLaunchKernelGGL(fa_bwd_dkdv_kernel<128>, grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL(fa_bwd_dkdv_kernel<64>, grid, 256, lds, st, a);
         else hipLaunchKernelGGL(fa_bwd_dkdv_kernel<32>, grid, 256, lds, st, a);
     }
     {
-        dim3 grid((max_q + 127) / 128, a.Hq, a.nseg);
+        dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
         if (D == 128) hipLaunchKernelGGL(fa_bwd_dq_kernel<128>, grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL(fa_bwd_dq_kernel<64>, grid, 256, lds, st, a);

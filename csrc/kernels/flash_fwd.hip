@@ -157,12 +157,212 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v2 (D = 64, 128): 8 waves x 32 query rows (BM = 256) share each K/V tile; one workgroup per CU,
+// two waves per SIMD.  VALU per MFMA is the limiter of the v1 loop (rocprof: 10.9 VALU/MFMA), so:
+//  * every LDS address is a per-lane register computed once (swizzle folded in) + a compile-time
+//    immediate: the K/V loop is unrolled x2 so both buffer bases are constants;
+//  * row max on raw scores with v_max3 (no canonicalising max), scale folded into one FMA;
+//  * lazy rescale: the running max only moves when a row max exceeds it by > 8 (log2 units), and
+//    the O / l rescale is skipped by a wave-uniform test otherwise (P <= 2^8 stays exact in fp32,
+//    representable in bf16);
+//  * lane^32 exchanges through v_permlane32_swap;
+//  * masking only on boundary tiles, as 1-2 compares against per-lane bounds.
+template <int D>
+struct FwdV2 {
+    static constexpr int NW = 8, BM = 32 * NW, KT = 64, TILE = KT * D * 2, NKS = D / 16, NT = D / 32;
+    static constexpr float TH = 8.f;
+};
+
+template <int D>
+__global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
+    using C = FwdV2<D>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
+    // dimension and causal work is issued heaviest-first across all heads (LPT balance)
+    const int seg = blockIdx.y, hq = blockIdx.x;
+    const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
+    const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
+    const int ntiles_q = (Lq + C::BM - 1) / C::BM;
+    const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
+    if (qt >= ntiles_q) return;
+    const int hk = hq / (a.Hq / a.Hkv);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
+    const int off = Lk - Lq;
+    const int qwg0 = qt * C::BM, qw0 = qwg0 + 32 * wave, myq = qw0 + lq;
+    const int qlast = min(qwg0 + C::BM - 1, Lq - 1);
+    int khi = Lk;
+    if (a.causal) khi = min(Lk, qlast + off + 1);
+    else if (a.window >= 0) khi = min(Lk, qlast + off + a.window + 1);
+    int klo = 0;
+    if (a.window >= 0) klo = max(0, qwg0 + off - a.window);
+    klo = (klo / C::KT) * C::KT;
+
+    // ---- per-lane LDS offsets (bytes, relative to a tile base) ----
+    int rowoff[C::NKS];  // K row fragment: row lq, cols 16ks + 8h
+#pragma unroll
+    for (int ks = 0; ks < C::NKS; ++ks) rowoff[ks] = lds_off<D>(lq, 16 * ks + 8 * h);
+    int troff[C::NT][2];  // V^T fragment (ld_tr): rows 4h + i/4 (+8), cols 32t + 16g + 4(i&3)
+    {
+        const int g = (lane >> 4) & 1, i = lane & 15;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) {
+            troff[t][0] = lds_off<D>(4 * h + (i >> 2), 32 * t + 16 * g + 4 * (i & 3));
+            troff[t][1] = lds_off<D>(4 * h + (i >> 2) + 8, 32 * t + 16 * g + 4 * (i & 3));
+        }
+    }
+    // K / V tiles by LDS-DMA (no staging registers); rows past the segment land as zeros
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    DmaTile<D, C::NW> tk, tv;
+    tk.init(wave_u, lane, a.k_tok);
+    tv.init(wave_u, lane, a.v_tok);
+    const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
+    const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
+#define SA_FWD_ISSUE(KT, BUFP)                                                                  \
+    do {                                                                                        \
+        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);            \
+        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + C::TILE, wave_u);  \
+    } while (0)
+
+    bf16x8 qf[C::NKS];
+    {
+        const u16* qp = a.q + (int64_t)(q0s + min(myq, Lq - 1)) * a.q_tok + (int64_t)hq * a.q_head;
+#pragma unroll
+        for (int ks = 0; ks < C::NKS; ++ks)
+            qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * h));
+    }
+    f32x16 o[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) o[t] = f32x16{};
+    float m = -INFINITY, l = 0.f;
+    const float c2 = a.scale_log2;
+
+    auto tile = [&](const char* K, int kt) {
+        const char* V = K + C::TILE;
+        f32x16 s[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+        for (int ks = 0; ks < C::NKS; ++ks)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                s[b] = mfma(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
+        // keep the K fragment reads one or two MFMAs ahead instead of hoisting all of them
+#pragma unroll
+        for (int i = 0; i < 2 * C::NKS; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        }
+        // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
+        const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
+                               (a.window >= 0 && (kt < qw0 + 31 + off - a.window ||
+                                                  (!a.causal && kt + C::KT - 1 > qw0 + off + a.window)));
+        if (need_mask) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
+                int hi = Lk - 1 - base;
+                if (a.causal) hi = min(hi, myq + off - base);
+                else if (a.window >= 0) hi = min(hi, myq + off + a.window - base);
+                const int lo = a.window >= 0 ? myq + off - a.window - base : -1;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
+            }
+        }
+        float mx = vmax3(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+        for (int j = 3; j < 15; j += 2) mx = vmax3(mx, s[0][j], s[0][j + 1]);
+        mx = vmax3(mx, s[0][15], s[1][0]);
+#pragma unroll
+        for (int j = 1; j < 15; j += 2) mx = vmax3(mx, s[1][j], s[1][j + 1]);
+        mx = vmax3(mx, s[1][15], s[1][15]);
+        const float mrow = max_xchg32(mx) * c2;
+        if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {  // rare after the first tiles
+            const float mnew = fmaxf(m, mrow);
+            const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) o[t][j] *= alpha;
+            m = mnew;
+        }
+        const float nm = m == -INFINITY ? 0.f : -m;
+        float rs = 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
+                s[b][j] = p;
+                rs += p;
+            }
+        l += sum_xchg32(rs);
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc(s[b], ss);
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int kb = (32 * b + 16 * ss) * D * 2;
+                    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
+                    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
+                    o[t] = mfma(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
+                }
+#pragma unroll
+        for (int i = 0; i < 4 * C::NT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+        }
+    };
+
+    char* buf0 = smem;
+    char* buf1 = smem + 2 * C::TILE;
+    if (klo < khi) SA_FWD_ISSUE(klo, buf0);
+    __syncthreads();
+    // pairs of tiles (buffer 0 then 1) so every LDS address is register + immediate; odd tail peeled
+    const int ntiles = khi > klo ? (khi - klo + C::KT - 1) / C::KT : 0;
+    int kt = klo;
+    for (int pr = 0; pr < ntiles / 2; ++pr, kt += 2 * C::KT) {
+        SA_FWD_ISSUE(kt + C::KT, buf1);
+        tile(buf0, kt);
+        __syncthreads();
+        if (kt + 2 * C::KT < khi) SA_FWD_ISSUE(kt + 2 * C::KT, buf0);
+        tile(buf1, kt + C::KT);
+        __syncthreads();
+    }
+    if (ntiles & 1) tile(buf0, kt);
+#undef SA_FWD_ISSUE
+    if (myq < Lq) {
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        u16* op = a.o + (int64_t)(q0s + myq) * a.o_tok + (int64_t)hq * a.o_head;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                u16x4 w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = f2bf(o[t][4 * g + j] * inv);
+                *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * h) = w;
+            }
+        if (h == 0)
+            a.lse[(int64_t)hq * a.lse_stride + q0s + myq] = l > 0.f ? (m + __log2f(l)) * 0.69314718055994530942f : INFINITY;
+    }
+}
+
 namespace sa_launch {
 void fa_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
+    if (D == 128 || D == 64) {
+        dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(64 * FwdV2<128>::NW);
+        if (D == 128) hipLaunchKernelGGL(fa_fwd_v2_kernel<128>, grid, block, 4 * FwdV2<128>::TILE, st, a);
+        else hipLaunchKernelGGL(fa_fwd_v2_kernel<64>, grid, block, 4 * FwdV2<64>::TILE, st, a);
+        return;
+    }
     dim3 grid((max_q + 127) / 128, a.Hq, a.nseg), block(256);
-    const size_t lds = 4 * 64 * D * 2;
-    if (D == 128) hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, block, lds, st, a);
-    else if (D == 64) hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, block, lds, st, a);
-    else hipLaunchKernelGGL(fa_fwd_kernel<32>, grid, block, lds, st, a);
+    hipLaunchKernelGGL(fa_fwd_kernel<32>, grid, block, 4 * 64 * 32 * 2, st, a);
 }
 }  // namespace sa_launch

@@ -57,7 +57,7 @@ void fa_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st);
 
 struct BwdArgs {
     const uint16_t* q; const uint16_t* k; const uint16_t* v; const uint16_t* dO;
-    const float* lse; float* delta;
+    const float* lse; float* delta; float* lse2;
     uint16_t* dq; uint16_t* dk; uint16_t* dv;
     int64_t q_tok, q_head, k_tok, k_head, v_tok, v_head, do_tok, do_head;
     int64_t dq_tok, dq_head, dk_tok, dk_head, dv_tok, dv_head, lse_stride;

@@ -75,6 +75,15 @@ def _obj_for(src: Path, flags: list[str]) -> Path:
     return BUILD / f"{src.stem}-{h.hexdigest()[:16]}.o"
 
 
+def _check_kernel_stubs(so: Path) -> None:
+    """Fail the build if a kernel launch references a host stub that was never emitted (seen with
+    hipcc when a template kernel's body trips its host pass): such a library imports but cannot load."""
+    r = subprocess.run(["nm", "-C", "--undefined-only", str(so)], capture_output=True, text=True)
+    missing = [ln.strip() for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        raise RuntimeError("kernel host stubs missing from the extension:\n" + "\n".join(missing))
+
+
 def _compile(src: Path, flags: list[str]) -> Path:
     obj = _obj_for(src, flags)
     if obj.exists():
@@ -148,6 +157,7 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    _check_kernel_stubs(Path(str(out) + ".tmp"))
     os.replace(str(out) + ".tmp", out)
     for old in BUILD.glob("link-*.stamp"):
         old.unlink()
