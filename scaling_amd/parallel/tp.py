@@ -66,14 +66,18 @@ def raw_shard(x: torch.Tensor, dim: int, size: int, rank: int) -> torch.Tensor:
 
 
 def raw_reduce_scatter_seq(x: torch.Tensor, size: int, group: Any) -> torch.Tensor:
-    """Reduce-scatter over the flattened token buffer; shape [b, s, ...] -> [b, s/size, ...]."""
+    """Sum over the TP group and keep this rank's 1/size of the tokens; [b, s, ...] -> [b, s/size, ...].
+
+    Operates on the flattened buffer (rank r keeps the r-th contiguous chunk), which is the partition
+    RCCL's reduce-scatter produces; the sequence-parallel region is token-wise so only the consistency
+    of scatter and gather matters (reference ``core/nn/linear/utils.py:270-310``)."""
     if size == 1:
         return x
     shape = list(x.shape)
     assert shape[1] % size == 0, "Sequence parallel size should be divisible by tensor parallel size"
     shape[1] //= size
     out = torch.empty(shape, dtype=x.dtype, device=x.device)
-    dist.reduce_scatter_tensor(out, x.contiguous(), group=group)
+    dist.reduce_scatter_tensor(out.view(-1), x.contiguous().view(-1), group=group)
     return out
 
 
@@ -83,7 +87,7 @@ def raw_gather_seq(x: torch.Tensor, size: int, group: Any) -> torch.Tensor:
     shape = list(x.shape)
     shape[1] *= size
     out = torch.empty(shape, dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    dist.all_gather_into_tensor(out.view(-1), x.contiguous().view(-1), group=group)
     return out
 
 

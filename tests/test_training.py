@@ -1,0 +1,92 @@
+"""End-to-end training on CPU/gloo of a tiny transformer: data pipeline -> 3D-parallel engine -> ZeRO-1
+optimizer -> checkpoint at step 6 -> resume must reproduce steps 7-10 exactly (reference:
+tests/transformer/test_training.py, which asserts diff_pct < 1e-10 after resume)."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from tests.dist_utils import free_port
+
+pytestmark = pytest.mark.cpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _make_data(prefix: Path) -> None:
+    sys.path.insert(0, str(ROOT))
+    from scaling_amd.core import MemoryMapDatasetBuilder
+
+    rng = np.random.RandomState(0)
+    with MemoryMapDatasetBuilder(prefix) as b:
+        for _ in range(300):
+            b.add(rng.randint(1, 1000, size=rng.randint(10, 300)))
+
+
+def _config(tmp: Path, mp: int, pp: int, world: int, **arch_over) -> dict:
+    topo = {"world_size": world, "model_parallel_size": mp, "pipe_parallel_size": pp, "micro_batch_size": 2,
+            "gradient_accumulation_steps": 2, "activation_checkpointing_type": arch_over.pop("checkpointing", "disabled"),
+            "sequence_parallel": arch_over.pop("sequence_parallel", False)}
+    arch = {"vocab_size": 1024, "sequence_length": 64, "hidden_size": 64, "num_attention_heads": 4, "num_layers": 2,
+            "precision": "float32", "dropout_embedding": 0.1, "dropout_attention_probs": 0.1,
+            "dropout_after_attention": 0.1, "dropout_after_mlp": 0.1, "masked_softmax": {"kernel": "torch"},
+            "norm_type": "rms", "mlp_type": "swiglu", "mlp_factor": 2.0, "weight_tying": False,
+            "attention_num_kv_heads": 2, "attention_qkv_in_one": False}
+    arch.update(arch_over)
+    return {
+        "topology": topo,
+        "optimizer": {"beta1": 0.9, "beta2": 0.99, "gradient_clipping": 1.0, "zero": True},
+        "learning_rate_scheduler": {"learning_rate": 0.01, "learning_rate_warmup_steps": 2,
+                                    "learning_rate_decay_iters": 10, "learning_rate_decay_style": "cosine"},
+        "embedding_learning_rate_scheduler": {"learning_rate": 0.001, "learning_rate_warmup_steps": 2,
+                                              "learning_rate_decay_iters": 10, "learning_rate_decay_style": "cosine"},
+        "training": {"use_separate_lr_on_embeddings": True},
+        "trainer": {"save_dir": str(tmp / "ckpt"), "save_interval": 6, "load_dir": str(tmp / "ckpt"),
+                    "train_iterations": 10, "assert_checkpoint_loaded": False},
+        "logger": {"log_level": "warning", "log_dir": str(tmp / "logs")},
+        "profiler": {"profile_steps": 2, "profile_start_at_step": 1},
+        "data": {"data_prefixes": [str(tmp / "data")], "blended_dataset": {"cache_directory": str(tmp)}},
+        "transformer_architecture": arch,
+    }
+
+
+def _run(tmp: Path, cfg: dict, world: int, tag: str) -> list:
+    spec = tmp / f"{tag}.json"
+    out = tmp / f"{tag}.out.json"
+    spec.write_text(json.dumps({"config": cfg, "out": str(out)}))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "tests" / "train_helper.py"), str(spec)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads(out.read_text())
+
+
+@pytest.mark.parametrize(
+    "mp,pp,world,extra",
+    [
+        (1, 1, 1, {}),
+        (1, 1, 2, {}),
+        (2, 1, 2, {}),
+        (1, 2, 2, {}),
+        (2, 1, 2, {"sequence_parallel": True}),
+        (1, 1, 1, {"checkpointing": "every_layer", "norm_type": "layernorm", "mlp_type": "default", "mlp_factor": 4.0,
+                   "weight_tying": True, "attention_num_kv_heads": None, "attention_qkv_in_one": True}),
+        (1, 2, 2, {"checkpointing": "every_pipe_stage", "weight_tying": True}),
+    ],
+)
+def test_train_and_resume_bit_exact(tmp_path, mp, pp, world, extra):
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, mp, pp, world, **extra)
+    full = _run(tmp_path, cfg, world, "full")
+    assert len(full) == 10
+    assert all(np.isfinite(m["training/loss"]) for m in full)
+    cfg["trainer"]["assert_checkpoint_loaded"] = True
+    resumed = _run(tmp_path, cfg, world, "resumed")
+    assert [m["training/loss"] for m in resumed] == [m["training/loss"] for m in full[-4:]]
+    assert (tmp_path / "ckpt" / "global_step6").is_dir()
+    # the profiler wrote its timings
+    assert any(p.name == "profile.json" for p in (tmp_path / "logs").rglob("profile.json"))
