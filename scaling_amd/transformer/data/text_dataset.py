@@ -100,7 +100,38 @@ class TextDataset(BaseDataset[TextDatasetItem, TextDatasetBatchBeforeSync, TextD
         s = self.memory_map.sizes() if callable(self.memory_map.sizes) else self.memory_map.sizes
         return np.asarray(s, dtype=np.int64)
 
+    def get_data_index_cache_filename_done(self, seed: int) -> str:
+        return self.get_data_index_cache_filename_stem(seed) + ".done"
+
+    def compute_data_index(self, seed: int) -> None:
+        """Legacy (MMIDIDX) item index: int32 (doc, start, end) triples per item plus a ``.done`` marker
+        (reference ``text_dataset.py:125-218``)."""
+        if self.seed is not None and self.seed == seed:
+            return
+        self.seed = seed
+        from .legacy_dataset import get_indexed_dataset_
+        from .legacy_dataset.indexed_dataset import Index
+
+        stem = self.get_data_index_cache_filename_stem(seed)
+        done = self.get_data_index_cache_filename_done(seed)
+        if not Path(done).is_file() and _rank() == 0:
+            order = np.arange(len(self.memory_map))
+            np.random.RandomState(seed=seed).shuffle(order)
+            from scaling_amd import _data  # type: ignore[attr-defined]
+
+            flat, pairs = _data.text_index(np.asarray(self.memory_map.sizes, dtype=np.int64), order.astype(np.int64),
+                                           int(self.sequence_length), False, 0)
+            flat.astype(np.int32).tofile(stem + ".bin")
+            Index.write(stem + ".idx", np.int32, pairs.reshape(-1, 2)[:, 1].tolist(), [0])
+            Path(done).write_text("True")
+        while not (Path(stem + ".bin").is_file() and Path(stem + ".idx").is_file() and Path(done).is_file()):
+            time.sleep(0.5)
+        self.data_item_index = get_indexed_dataset_(stem, "mmap", True)  # type: ignore[assignment]
+
     def set_seed(self, seed: int, shuffle: bool = True) -> None:
+        if self.legacy_dataset:
+            self.compute_data_index(seed)
+            return
         if self.seed is not None and self.seed == seed:
             return
         self.seed = seed
