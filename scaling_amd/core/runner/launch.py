@@ -35,6 +35,9 @@ def main(argv: list[str] | None = None) -> int:
     host = hosts[args.node_rank]
     world = sum(len(v) for v in pool.values())
     first_rank = sum(len(pool[h]) for h in hosts[: args.node_rank])
+    if not pool[host]:
+        print(f"[launch] no slots for host {host} in the resource pool (e.g. 'host slots=8')", file=sys.stderr)
+        return 2
     procs: list[subprocess.Popen[Any]] = []
     for i, slot in enumerate(pool[host]):
         env = dict(os.environ)

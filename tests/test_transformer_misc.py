@@ -1,0 +1,132 @@
+"""Transformer suite pieces: inference (cached == uncached generation, samplers, checkpoint round trip),
+tokenizer, FLOP accounting, embedding head, image encoder, determined hparam mapping, MLP example.
+(Reference: tests/transformer/test_inference.py, test_tokenizer, test_utils.py.)"""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.cpu
+REF = Path("/root/reference/tests/transformer/files")
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _arch(**kw):
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+
+    d = dict(vocab_size=128, hidden_size=64, num_layers=2, num_attention_heads=4, sequence_length=64, norm_type="rms",
+             mlp_type="swiglu", mlp_factor=2.0, precision="float32", attention_num_kv_heads=2,
+             attention_qkv_in_one=False, weight_tying=False, relative_position_embedding_type="rotary_complex")
+    d.update(kw)
+    return TransformerArchitectureConfig(**d)
+
+
+@pytest.mark.parametrize("kw", [{}, {"weight_tying": True, "norm_type": "layernorm", "mlp_type": "default",
+                                     "mlp_factor": 4.0, "attention_num_kv_heads": None, "attention_qkv_in_one": True,
+                                     "relative_position_embedding_type": "rotary"}])
+def test_generation_cached_equals_uncached(kw):
+    from scaling_amd.transformer.inference import TransformerInferenceModule
+    from scaling_amd.transformer.model.model import get_transformer_layer_specs
+
+    torch.manual_seed(0)
+    m = TransformerInferenceModule(get_transformer_layer_specs(_arch(**kw)), devices=("cpu",))
+    a = m.generate(8, input_tokens=[1, 2, 3, 4, 5], stop_tokens=[127], use_cache=True)
+    b = m.generate(8, input_tokens=[1, 2, 3, 4, 5], stop_tokens=[127], use_cache=False)
+    assert a.completion_tokens == b.completion_tokens
+    torch.testing.assert_close(a.completion_logits, b.completion_logits, rtol=1e-4, atol=1e-4)
+    logits = m.logits(input_tokens=[1, 2, 3])
+    assert logits.shape == (3, 128)
+
+
+def test_samplers():
+    from scaling_amd.transformer.inference import sample_argmax, sample_temperature, top_k_transform, top_p_transform
+
+    torch.manual_seed(0)
+    logits = torch.randn(1, 3, 50)
+    assert sample_argmax(logits).item() == logits[0, -1].argmax().item()
+    assert 0 <= sample_temperature(logits, 0.7).item() < 50
+    k = top_k_transform(logits[0, -1], 5)
+    assert torch.isfinite(k).sum() == 5
+    p = top_p_transform(logits[0, -1], 0.5)
+    assert 1 <= torch.isfinite(p).sum() < 50
+
+
+@pytest.mark.skipif(not (REF / "llama2-tokenizer.json").exists(), reason="reference tokenizer not mounted")
+def test_tokenizer_roundtrip_and_no_prefix_variant():
+    from scaling_amd.transformer.tokenizer import load_tokenizers
+
+    tok, tok_nps = load_tokenizers(REF / "llama2-tokenizer.json")
+    assert len(tok) == 32000 and tok.eos_token_id == 2
+    ids = tok.encode("Hello world")
+    assert tok.decode(ids).strip() == "Hello world"
+    assert tok_nps.encode("Hello")[0] != tok.encode("Hello")[0]  # no leading-space variant
+
+
+def test_flop_accounting():
+    from scaling_amd.core import TopologyConfig
+    from scaling_amd.transformer.utils.get_tflops import (get_model_flop_utilization_palm, get_tflops_aleph_alpha,
+                                                          get_tflops_bloom, get_tflops_electra, get_tflops_megatron)
+
+    class T:
+        config = TopologyConfig(global_rank=0, world_size=8, model_parallel_size=1, pipe_parallel_size=1,
+                                micro_batch_size=4, gradient_accumulation_steps=2)
+
+    a = _arch(hidden_size=4096, num_layers=32, num_attention_heads=32, vocab_size=32000, sequence_length=4096,
+              attention_num_kv_heads=None, attention_qkv_in_one=True)
+    for f in (get_tflops_aleph_alpha, get_tflops_electra, get_tflops_bloom):
+        assert f(1.0, T, a) > 0
+    mega = get_tflops_megatron(6_700_000_000, 1.0, T, a)
+    # 6 N tokens + attention; tokens = gbs * seq
+    tokens = 64 * 4096
+    assert abs(mega - (6 * 6.7e9 * tokens + tokens * 4096 * 4096 * 32 * 60) / 8e12) / mega < 1e-9
+    assert get_model_flop_utilization_palm(1.0, 6_700_000_000, T, a) >= 0.0
+
+
+def test_embedding_head_pooling():
+    from scaling_amd.transformer.model.layers import TransformerEmbeddingHead
+
+    e = torch.randn(2, 5, 8)
+    w = torch.tensor([[1, 1, 0, 0, 0], [0, 0, 0, 0, 0]], dtype=torch.float)
+    out = TransformerEmbeddingHead.weighted_mean_pooling(e, w)
+    ref0 = (e[0, 0] * 1 + e[0, 1] * 2) / 3
+    torch.testing.assert_close(out[0], ref0)
+
+
+def test_image_encoder_token_shape():
+    from scaling_amd.transformer.model.image_encoder import ClipModifiedResNet, clip_transform
+
+    torch.manual_seed(0)
+    net = ClipModifiedResNet(layers=[1, 1, 1, 1], num_init_channels=8).eval()
+    with torch.no_grad():
+        tok = net(torch.randn(1, 3, 96, 96))
+    assert tok.shape == (1, 9, 8 * 8 * 4)  # 96/32 = 3 -> 9 tokens, width 8*8*4
+    from PIL import Image
+
+    t = clip_transform((32, 32))(Image.new("RGB", (40, 50), (255, 0, 0)))
+    assert t.shape == (3, 32, 32)
+
+
+def test_determined_hparams_mapping():
+    from scaling_amd.transformer.train_determined import hparams_to_overrides
+
+    o = hparams_to_overrides({"layout": {"global_batch_size": 8, "sequence_length": 64, "target_train_tokens": 5120,
+                                         "warmup_tokens": 512, "model_parallel_size": 2, "kernel": "torch"}})
+    assert o["trainer"]["train_iterations"] == 10
+    assert o["learning_rate_scheduler"]["learning_rate_warmup_steps"] == 1
+    assert o["topology"]["model_parallel_size"] == 2
+    assert o["transformer_architecture"]["masked_softmax"] == {"kernel": "torch"}
+
+
+def test_mlp_example_trains(tmp_path):
+    cfg = (ROOT / "examples/mlp_example/config.yml").read_text()
+    cfg = cfg.replace('"train_iterations": 50', '"train_iterations": 30').replace('"master_port": 29511', '"master_port": 29641')
+    cfg = cfg.replace('"save_dir": ".checkpoints_mlp"', f'"save_dir": "{tmp_path}/ck"')
+    cfg = cfg.replace('"log_dir": "debug_logs"', f'"log_dir": "{tmp_path}/logs"')
+    (tmp_path / "c.yml").write_text(cfg)
+    r = subprocess.run([sys.executable, "-m", "examples.mlp_example.run", str(tmp_path / "c.yml")], cwd=str(ROOT),
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, PYTHONPATH=str(ROOT)))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "completed step 30" in r.stdout + r.stderr
