@@ -27,8 +27,9 @@ void check_cuda(const at::Tensor& t, const char* name) {
 }
 
 // ------------------------------------------------------------------ norms
+// res given: normalises s = x + res and also returns s (fused residual add)
 std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
-                                 double eps, bool layer) {
+                                 double eps, bool layer, const c10::optional<at::Tensor>& res) {
     check_cuda(x, "x");
     check_cuda(w, "weight");
     const int64_t H = x.size(-1);
@@ -46,14 +47,24 @@ std::vector<at::Tensor> norm_fwd(const at::Tensor& x, const at::Tensor& w, const
         check_cuda(*b, "bias");
         bp = b->data_ptr();
     }
+    at::Tensor sum = at::empty({0}, x.options());
+    const void* rp = nullptr;
+    if (res.has_value()) {
+        check_cuda(*res, "residual");
+        TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(), "norm: residual mismatch");
+        sum = at::empty_like(x);
+        rp = res->data_ptr();
+    }
     sa_launch::norm_fwd(dt(x), layer, x.data_ptr(), w.data_ptr(), bp, y.data_ptr(),
                         layer ? mean.data_ptr<float>() : nullptr, rstd.data_ptr<float>(), rows, (int)H, (float)eps,
-                        cur_stream());
-    return {y, mean, rstd};
+                        cur_stream(), rp, rp ? sum.data_ptr() : nullptr);
+    return {y, mean, rstd, sum};
 }
 
+// dadd given: dx = norm_bwd(dy) + dadd (fused residual-gradient add)
 std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& w,
-                                 const at::Tensor& mean, const at::Tensor& rstd, bool layer) {
+                                 const at::Tensor& mean, const at::Tensor& rstd, bool layer,
+                                 const c10::optional<at::Tensor>& dadd) {
     check_cuda(dy, "dy");
     check_cuda(x, "x");
     const int64_t H = x.size(-1);
@@ -62,15 +73,20 @@ std::vector<at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x, cons
     auto dx = at::empty_like(x);
     auto dw = at::empty_like(w);
     auto db = layer ? at::empty_like(w) : at::empty({0}, w.options());
-    const int nw = sa_launch::norm_bwd_waves(rows);
-    auto part = at::empty({(layer ? 2 : 1) * (int64_t)nw * H}, x.options().dtype(at::kFloat));
+    auto part = at::empty({sa_launch::norm_bwd_scratch(rows, (int)H, layer)}, x.options().dtype(at::kFloat));
+    const void* ap = nullptr;
+    if (dadd.has_value()) {
+        check_cuda(*dadd, "dadd");
+        TORCH_CHECK(dadd->is_contiguous() && dadd->numel() == x.numel() && dadd->scalar_type() == x.scalar_type(),
+                    "norm_bwd: dadd mismatch");
+        ap = dadd->data_ptr();
+    }
     sa_launch::norm_bwd(dt(x), layer, dy.data_ptr(), x.data_ptr(), w.data_ptr(),
                         layer ? mean.data_ptr<float>() : nullptr, rstd.data_ptr<float>(), dx.data_ptr(),
                         dw.data_ptr(), layer ? db.data_ptr() : nullptr, part.data_ptr<float>(), rows, (int)H,
-                        cur_stream());
+                        cur_stream(), ap);
     return {dx, dw, db};
 }
-
 
 // ------------------------------------------------------------------ swiglu
 // z: [..., 2F] (a | b halves) or separate a/b with equal row stride
@@ -107,15 +123,25 @@ std::vector<at::Tensor> swiglu_bwd(const at::Tensor& dy, const at::Tensor& a, co
 }
 
 // ------------------------------------------------------------------ rope
-// x: [T, nh, hd] (any token/head stride, unit element stride) -> contiguous [T, nh, hd]
+// x: [T, nh, hd] (any token/head stride, unit element stride) -> out (given: same shape, any strides, may be x
+// itself for an in-place rotation; else a new contiguous [T, nh, hd])
 at::Tensor rope(const at::Tensor& x, const at::Tensor& cosb, const at::Tensor& sinb, const c10::optional<at::Tensor>& pos,
-                int64_t rot_dim, int64_t seq_len, bool interleaved, bool inverse) {
+                int64_t rot_dim, int64_t seq_len, bool interleaved, bool inverse, const c10::optional<at::Tensor>& out_) {
     TORCH_CHECK(x.is_cuda() && x.dim() == 3 && x.stride(2) == 1, "rope: x must be [T, nh, hd] with unit last stride");
     TORCH_CHECK(cosb.scalar_type() == at::kFloat && cosb.is_contiguous() && sinb.is_contiguous(), "rope: fp32 tables");
     const int64_t T = x.size(0), nh = x.size(1), hd = x.size(2);
     TORCH_CHECK(rot_dim % 2 == 0 && rot_dim <= hd && cosb.size(-1) == rot_dim / 2, "rope: bad rotary dims");
     const at::DeviceGuard g(x.device());
-    auto out = at::empty({T, nh, hd}, x.options());
+    at::Tensor out;
+    if (out_.has_value()) {
+        out = *out_;
+        TORCH_CHECK(out.sizes() == x.sizes() && out.stride(2) == 1 && out.scalar_type() == x.scalar_type(),
+                    "rope: out must match x with unit last stride");
+        TORCH_CHECK(out.data_ptr() == x.data_ptr() ? out.strides() == x.strides() : true,
+                    "rope: in-place output must have the input's strides");
+    } else {
+        out = at::empty({T, nh, hd}, x.options());
+    }
     const int64_t* pp = nullptr;
     at::Tensor pc;
     if (pos.has_value()) {
@@ -123,9 +149,9 @@ at::Tensor rope(const at::Tensor& x, const at::Tensor& cosb, const at::Tensor& s
         TORCH_CHECK(pc.numel() == T, "rope: position ids must have one entry per token");
         pp = pc.data_ptr<int64_t>();
     }
-    sa_launch::rope(dt(x), interleaved, x.data_ptr(), x.stride(0), x.stride(1), out.data_ptr(), cosb.data_ptr<float>(),
-                    sinb.data_ptr<float>(), pp, T, (int)nh, (int)hd, (int)rot_dim, (int)seq_len, inverse ? -1.f : 1.f,
-                    cur_stream());
+    sa_launch::rope(dt(x), interleaved, x.data_ptr(), x.stride(0), x.stride(1), out.data_ptr(), out.stride(0),
+                    out.stride(1), cosb.data_ptr<float>(), sinb.data_ptr<float>(), pp, T, (int)nh, (int)hd,
+                    (int)rot_dim, (int)seq_len, inverse ? -1.f : 1.f, cur_stream());
     return out;
 }
 
@@ -255,15 +281,24 @@ std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const a
 }
 std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_q, const at::Tensor& cu_k,
-                               int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window) {
+                               int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window,
+                               const c10::optional<at::Tensor>& dq_out, const c10::optional<at::Tensor>& dk_out,
+                               const c10::optional<at::Tensor>& dv_out) {
+    // d*_out: write the gradients into caller-provided strided views (e.g. slices of one dQKV buffer)
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(o, "o");
     auto dO = dout.contiguous();
     check_qkv(dO, "dout");
     const int64_t D = q.size(2), T = q.size(0), H = q.size(1), Tk = k.size(0), Hk = k.size(1);
     const at::DeviceGuard g(q.device());
-    auto dq = at::empty({T, H, D}, q.options());
-    auto dk = at::empty({Tk, Hk, D}, k.options());
-    auto dv = at::empty({Tk, Hk, D}, v.options());
+    auto take = [](const c10::optional<at::Tensor>& t, const at::Tensor& like, const char* n) {
+        if (!t.has_value()) return at::empty(like.sizes(), like.options());
+        TORCH_CHECK(t->sizes() == like.sizes() && t->scalar_type() == like.scalar_type(), "fa_bwd: ", n, " shape/dtype");
+        check_qkv(*t, n);
+        return *t;
+    };
+    auto dq = take(dq_out, q, "dq_out");
+    auto dk = take(dk_out, k, "dk_out");
+    auto dv = take(dv_out, v, "dv_out");
     auto delta = at::empty({H, T}, q.options().dtype(at::kFloat));
     auto lse2 = at::empty({H, T}, q.options().dtype(at::kFloat));
     BwdArgs a{};
@@ -286,11 +321,11 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "scaling_amd CDNA4 (gfx950) HIP kernels";
-    m.def("norm_fwd", &norm_fwd, "RMSNorm/LayerNorm forward");
-    m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward");
+    m.def("norm_fwd", &norm_fwd, "RMSNorm/LayerNorm forward (optional fused residual add)", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("layer"), py::arg("res") = py::none());
+    m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
-    m.def("rope", &rope, "rotary embedding (fwd / inverse)");
+    m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());
     m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
     m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
     m.def("embed_fwd", &embed_fwd, "vocab-parallel embedding forward");
@@ -299,5 +334,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sumsq_", &sumsq_, "sum of squares + non-finite count");
     m.def("cast_scale_", &cast_scale_, "y = cast(x * scale)");
     m.def("fa_fwd", &fa_fwd, "flash attention forward");
-    m.def("fa_bwd", &fa_bwd, "flash attention backward");
+    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none());
 }

@@ -9,10 +9,12 @@ enum SaDType { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
 namespace sa_launch {
 // norm.hip
 void norm_fwd(int dtype, bool layer, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-              int64_t rows, int H, float eps, hipStream_t st);
-int norm_bwd_waves(int64_t rows);
+              int64_t rows, int H, float eps, hipStream_t st, const void* res = nullptr, void* sum_out = nullptr);
+int norm_bwd_waves(int64_t rows, int H);
+int64_t norm_bwd_scratch(int64_t rows, int H, bool layer);
 void norm_bwd(int dtype, bool layer, const void* dy, const void* x, const void* w, const float* mean,
-              const float* rstd, void* dx, void* dw, void* db, float* part, int64_t rows, int H, hipStream_t st);
+              const float* rstd, void* dx, void* dw, void* db, float* part, int64_t rows, int H, hipStream_t st,
+              const void* dadd = nullptr);
 }  // namespace sa_launch
 
 namespace sa_launch {
@@ -20,9 +22,9 @@ namespace sa_launch {
 void swiglu_fwd(int dtype, const void* a, const void* b, int64_t lda, void* out, int64_t rows, int F, hipStream_t st);
 void swiglu_bwd(int dtype, const void* dy, const void* a, const void* b, int64_t lda, void* da, void* db, int64_t ldd,
                 int64_t rows, int F, hipStream_t st);
-void rope(int dtype, bool interleaved, const void* x, int64_t tok_stride, int64_t head_stride, void* out,
-          const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd, int seq_len,
-          float sign, hipStream_t st);
+void rope(int dtype, bool interleaved, const void* x, int64_t x_tok, int64_t x_head, void* out, int64_t o_tok,
+          int64_t o_head, const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd,
+          int seq_len, float sign, hipStream_t st);
 }  // namespace sa_launch
 
 namespace sa_launch {

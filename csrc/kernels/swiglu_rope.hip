@@ -53,38 +53,104 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ d
 }
 
 // ------------------------------------------------------------------ RoPE
-// x: [T, nh, hd] with arbitrary token/head strides (elements); out: contiguous [T, nh, hd].
+// x, out: [T, nh, hd] with arbitrary token/head strides (elements, unit element stride); out may alias x
+// (every work item reads its elements before writing the same elements), which the fused attention
+// backward uses to rotate dq/dk in place inside the dQKV buffer.
 // table: fp32 cos/sin [max_pos, rd/2] (NeoX: pair (i, i+rd/2); complex: pair (2i, 2i+1)).
 // sign = +1 forward, -1 backward (rotation transpose). Dims >= rd are copied through.
+struct RopeArgs {
+    int64_t xt, xh, ot, oh;  // token / head strides of x and out
+    const float* cosb;
+    const float* sinb;
+    const int64_t* pos;
+    int T, nh, hd, rd, seq_len;
+    float sign;
+};
+
+// Vector path: one work item = 8 pair slots of one (token, head) row — NeoX: elements p..p+7 and
+// half+p..half+p+7 (two 16 B loads); complex: elements e..e+7 (four pairs, one 16 B load); the
+// pass-through tail [rd, hd) moves in 8-element chunks.  Needs 16 B aligned rows (checked on host).
+template <typename T, bool IL>
+__global__ __launch_bounds__(256) void rope_v8_kernel(const T* __restrict__ x, T* __restrict__ out, RopeArgs a) {
+    const int half = a.rd / 2;
+    const int rc = IL ? a.rd / 8 : half / 8;  // rotating chunks per row
+    const int CR = rc + (a.hd - a.rd) / 8;
+    const int n = a.T * a.nh * CR;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int row = i / CR, c = i - row * CR;
+        const int t = row / a.nh, h = row - t * a.nh;
+        const T* xr = x + t * a.xt + h * a.xh;
+        T* orow = out + t * a.ot + h * a.oh;
+        if (c < rc) {
+            const int64_t ps = a.pos ? a.pos[t] : (t % a.seq_len);
+            const float* cb = a.cosb + ps * half;
+            const float* sb = a.sinb + ps * half;
+            if (!IL) {
+                const int p = c * 8;
+                float x0[8], x1[8], cs[8], sn[8], o0[8], o1[8];
+                V8<T>::ld(xr + p, x0);
+                V8<T>::ld(xr + half + p, x1);
+                V8<float>::ld(cb + p, cs);
+                V8<float>::ld(sb + p, sn);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float sj = sn[j] * a.sign;
+                    o0[j] = x0[j] * cs[j] - x1[j] * sj;
+                    o1[j] = x1[j] * cs[j] + x0[j] * sj;
+                }
+                V8<T>::st(orow + p, o0);
+                V8<T>::st(orow + half + p, o1);
+            } else {
+                const int e = c * 8;
+                float v[8], o[8];
+                V8<T>::ld(xr + e, v);
+                const f32x4 cs = *reinterpret_cast<const f32x4*>(cb + e / 2);
+                const f32x4 sn = *reinterpret_cast<const f32x4*>(sb + e / 2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float sj = sn[j] * a.sign;
+                    o[2 * j] = v[2 * j] * cs[j] - v[2 * j + 1] * sj;
+                    o[2 * j + 1] = v[2 * j + 1] * cs[j] + v[2 * j] * sj;
+                }
+                V8<T>::st(orow + e, o);
+            }
+        } else {
+            const int e = a.rd + (c - rc) * 8;
+            float v[8];
+            V8<T>::ld(xr + e, v);
+            V8<T>::st(orow + e, v);
+        }
+    }
+}
+
+// Scalar fallback (odd rotary dims / unaligned views): one thread per (token, head, pair).
 template <typename T, bool INTERLEAVED>
-__global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, int64_t tok_stride, int64_t head_stride,
-                                                   T* __restrict__ out, const float* __restrict__ cosb,
-                                                   const float* __restrict__ sinb, const int64_t* __restrict__ pos,
-                                                   int64_t T_, int nh, int hd, int rd, int seq_len, float sign) {
-    // one thread per (token, head, pair)
-    const int half = rd / 2;
-    const int pairs = half + (hd - rd + 1) / 2;  // rotated pairs + pass-through element pairs
-    const int64_t n = T_ * nh * pairs;
+__global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* __restrict__ out, RopeArgs a) {
+    const int half = a.rd / 2;
+    const int pairs = half + (a.hd - a.rd + 1) / 2;  // rotated pairs + pass-through element pairs
+    const int64_t n = (int64_t)a.T * a.nh * pairs;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int p = (int)(i % pairs);
         const int64_t th = i / pairs;
-        const int h = (int)(th % nh);
-        const int64_t t = th / nh;
-        const T* xr = x + t * tok_stride + (int64_t)h * head_stride;
-        T* orow = out + (t * nh + h) * hd;
+        const int h = (int)(th % a.nh);
+        const int64_t t = th / a.nh;
+        const T* xr = x + t * a.xt + (int64_t)h * a.xh;
+        T* orow = out + t * a.ot + (int64_t)h * a.oh;
         if (p < half) {
-            const int64_t ps = pos ? pos[t] : (t % seq_len);
-            const float c = cosb[ps * half + p];
-            const float s = sinb[ps * half + p] * sign;
+            const int64_t ps = a.pos ? a.pos[t] : (t % a.seq_len);
+            const float c = a.cosb[ps * half + p];
+            const float s = a.sinb[ps * half + p] * a.sign;
             const int i0 = INTERLEAVED ? 2 * p : p;
             const int i1 = INTERLEAVED ? 2 * p + 1 : p + half;
             const float x0 = IO<T>::ld(xr, i0), x1 = IO<T>::ld(xr, i1);
             IO<T>::st(orow, i0, x0 * c - x1 * s);
             IO<T>::st(orow, i1, x1 * c + x0 * s);
         } else {
-            const int j = rd + 2 * (p - half);
-            orow[j] = xr[j];
-            if (j + 1 < hd) orow[j + 1] = xr[j + 1];
+            const int j = a.rd + 2 * (p - half);
+            const T v0 = xr[j];
+            const T v1 = j + 1 < a.hd ? xr[j + 1] : v0;
+            orow[j] = v0;
+            if (j + 1 < a.hd) orow[j + 1] = v1;
         }
     }
 }
@@ -108,12 +174,28 @@ void swiglu_bwd(int dtype, const void* dy, const void* a, const void* b, int64_t
     else if (dtype == DT_F16) hipLaunchKernelGGL(swiglu_bwd_kernel<f16>, g, 256, 0, st, (const f16*)dy, (const f16*)a, (const f16*)b, lda, (f16*)da, (f16*)db, ldd, rows, F);
     else hipLaunchKernelGGL(swiglu_bwd_kernel<float>, g, 256, 0, st, (const float*)dy, (const float*)a, (const float*)b, lda, (float*)da, (float*)db, ldd, rows, F);
 }
-void rope(int dtype, bool interleaved, const void* x, int64_t tok_stride, int64_t head_stride, void* out,
-          const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd, int seq_len,
-          float sign, hipStream_t st) {
+void rope(int dtype, bool interleaved, const void* x, int64_t x_tok, int64_t x_head, void* out, int64_t o_tok,
+          int64_t o_head, const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd,
+          int seq_len, float sign, hipStream_t st) {
+    const RopeArgs a{x_tok, x_head, o_tok, o_head, cosb, sinb, pos, (int)T_, nh, hd, rd, seq_len, sign};
+    const int vec_elems = dtype == DT_F32 ? 4 : 8;  // 16 B
+    const bool aligned = ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0) && x_tok % vec_elems == 0 &&
+                         x_head % vec_elems == 0 && o_tok % vec_elems == 0 && o_head % vec_elems == 0;
+    const bool vec = aligned && hd % 8 == 0 && (interleaved ? rd % 8 == 0 : rd % 16 == 0) &&
+                     T_ * nh * (hd / 8) < (int64_t)INT32_MAX;
+    if (vec) {
+        const int CR = (interleaved ? rd / 8 : rd / 16) + (hd - rd) / 8;
+        const int g = grid_for(T_ * nh * CR);
+#define SA_ROPE(TT, IL) hipLaunchKernelGGL((rope_v8_kernel<TT, IL>), g, 256, 0, st, (const TT*)x, (TT*)out, a)
+        if (dtype == DT_BF16) { if (interleaved) SA_ROPE(u16, true); else SA_ROPE(u16, false); }
+        else if (dtype == DT_F16) { if (interleaved) SA_ROPE(f16, true); else SA_ROPE(f16, false); }
+        else { if (interleaved) SA_ROPE(float, true); else SA_ROPE(float, false); }
+#undef SA_ROPE
+        return;
+    }
     const int pairs = rd / 2 + (hd - rd + 1) / 2;
     const int g = grid_for(T_ * nh * pairs);
-#define SA_ROPE(TT, IL) hipLaunchKernelGGL((rope_kernel<TT, IL>), g, 256, 0, st, (const TT*)x, tok_stride, head_stride, (TT*)out, cosb, sinb, pos, T_, nh, hd, rd, seq_len, sign)
+#define SA_ROPE(TT, IL) hipLaunchKernelGGL((rope_kernel<TT, IL>), g, 256, 0, st, (const TT*)x, (TT*)out, a)
     if (dtype == DT_BF16) { if (interleaved) SA_ROPE(u16, true); else SA_ROPE(u16, false); }
     else if (dtype == DT_F16) { if (interleaved) SA_ROPE(f16, true); else SA_ROPE(f16, false); }
     else { if (interleaved) SA_ROPE(float, true); else SA_ROPE(float, false); }

@@ -244,18 +244,43 @@ class ParallelSelfAttention(torch.nn.Module):
     # ------------------------------------------------------------------ projections
     def _project(self, x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         """Returns token-major q [T, nq, hd], k/v [T, nkv, hd] (possibly strided views)."""
+        return self._project_base(x)[:3]
+
+    def _project_base(self, x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+        """q, k, v views plus the single GEMM output they tile."""
         b, s, _ = x.shape
         T = b * s
         hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
         if self.qkv_in_one:
-            qkv = self.query_key_value(x).view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
-            return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :]
-        out = fused_column_linear(x, [self.query, self.key, self.value], self.topology)
-        out = out.view(T, nq * hd + 2 * nkv * hd)
+            base = self.query_key_value(x)
+            qkv = base.view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
+            return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :], base
+        base = fused_column_linear(x, [self.query, self.key, self.value], self.topology)
+        out = base.view(T, nq * hd + 2 * nkv * hd)
         q = out[:, : nq * hd].view(T, nq, hd)
         k = out[:, nq * hd : (nq + nkv) * hd].view(T, nkv, hd)
         v = out[:, (nq + nkv) * hd :].view(T, nkv, hd)
-        return q, k, v
+        return q, k, v, base
+
+    def _fused_rope_attention(self, base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                              position_ids: Optional[torch.Tensor], s: int, cumulative_seq_lengths: torch.Tensor,
+                              max_seq_length: Optional[int]) -> Optional[torch.Tensor]:
+        """RoPE + flash attention as one autograd node writing dQKV in place (None if not applicable)."""
+        nl = self.num_local_attention_heads
+        re = self.rotary_embedding
+        if re is None or not self.use_flash_attention or self.key_query_norm:
+            return None
+        if nl > 0 and nl != self.num_attention_heads:
+            return None
+        if self.lora_config is not None and not self.lora_merged_state:
+            return None
+        if self.dropout_attention_probs > 0.0 and self.training:
+            return None
+        pos = position_ids.reshape(-1) if position_ids is not None else None
+        return attn_ops.rope_flash_attention(
+            base, q, k, v, re.cos_table, re.sin_table, pos, re.dimensions, s, re.interleaved, cumulative_seq_lengths,
+            max_seq_length if max_seq_length is not None else s, self.scaling_factor, self.causal,
+            self.local_attention_window_size if nl > 0 else None)
 
     def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
         assert self.lora_config is not None
@@ -289,7 +314,11 @@ class ParallelSelfAttention(torch.nn.Module):
         b, s, _ = x.shape
         T = b * s
         hd = self.hidden_size_per_attention_head
-        q, k, v = self._project(x)
+        q, k, v, base = self._project_base(x)
+        if not use_cache and not reset_cache and cumulative_seq_lengths_key is None:
+            fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length)
+            if fused is not None:
+                return self._output(fused.reshape(b, s, -1))
         if self.lora_config is not None and not self.lora_merged_state:
             q, k, v = self.apply_lora(x, q, k, v)
         if self.key_query_norm:
@@ -352,6 +381,9 @@ class ParallelSelfAttention(torch.nn.Module):
                 cumulative_seq_lengths_key=None if Tk == T else cumulative_seq_lengths_key,
             )
 
+        return self._output(hidden)
+
+    def _output(self, hidden: torch.Tensor) -> torch.Tensor:
         dense_lora = None
         if self.lora_config and not self.lora_merged_state and LoRAModuleType.DENSE in self.lora_config.parallel_modules:
             dense_lora = self.lora_modules[f"dense_{self.lora_config.name}"](

@@ -64,6 +64,69 @@ class _FlashAttn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None, None
 
 
+def _spec(t: torch.Tensor, base: torch.Tensor) -> tuple:
+    return (tuple(t.shape), tuple(t.stride()), t.storage_offset() - base.storage_offset())
+
+
+def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
+    shape, stride, off = spec
+    return base.as_strided(shape, stride, base.storage_offset() + off)
+
+
+class _RopeFlashAttn(torch.autograd.Function):
+    """RoPE on q/k + flash attention over views of ONE projection output (``base``).
+
+    Backward allocates ``dbase`` once: the attention backward writes dq/dk/dv straight into its q/k/v
+    slices and the inverse rotation runs in place there, so no per-slice gradient buffers, zero-fills,
+    slice copies or gradient sums are materialised (autograd's view backward would do all of those)."""
+
+    @staticmethod
+    def forward(ctx: Any, base, specs, cos, sin, pos, rot_dim, seq_len, interleaved, cu_q, cu_k, max_q, max_k, scale,
+                causal, window):  # type: ignore[override]
+        qi, ki, vi = (_view(base, sp) for sp in specs)
+        q = ext().rope(qi, cos, sin, pos, rot_dim, seq_len, interleaved, False)
+        k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
+        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window)
+        ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
+        ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window)
+        return o
+
+    @staticmethod
+    def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
+        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
+        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window = ctx.cfg
+        dbase = torch.empty_like(base)
+        dq, dk, dv = (_view(dbase, sp) for sp in specs)
+        v = _view(base, specs[2])
+        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv)
+        ext().rope(dq, cos, sin, pos, rot_dim, seq_len, interleaved, True, dq)
+        ext().rope(dk, cos, sin, pos, rot_dim, seq_len, interleaved, True, dk)
+        return (dbase,) + (None,) * 14
+
+
+def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor,
+                         sin: torch.Tensor, pos: Optional[torch.Tensor], rot_dim: int, seq_len: int, interleaved: bool,
+                         cu_seqlens: torch.Tensor, max_seqlen: int, softmax_scale: float, causal: bool = True,
+                         window: Optional[int] = None) -> Optional[torch.Tensor]:
+    """Fused RoPE + flash attention for q/k/v that are views tiling ``base`` exactly (the QKV GEMM output).
+
+    Returns None when the fused path does not apply (CPU tensors, layouts that do not tile ``base``); the
+    caller then runs rope and :func:`flash_attention` separately."""
+    if not (use_native(base) and base.is_contiguous() and base.dtype == torch.bfloat16):
+        return None
+    if q.numel() + k.numel() + v.numel() != base.numel():
+        return None
+    for t in (q, k, v):
+        if t.untyped_storage().data_ptr() != base.untyped_storage().data_ptr():
+            return None
+    specs = (_spec(q, base), _spec(k, base), _spec(v, base))
+    cq = cu_seqlens.to(torch.int32)
+    p = None if pos is None else pos.reshape(-1).long()
+    win = -1 if window is None else int(window)
+    return _RopeFlashAttn.apply(base, specs, cos, sin, p, int(rot_dim), int(seq_len), bool(interleaved), cq, cq,
+                                int(max_seqlen), int(max_seqlen), float(softmax_scale), bool(causal), win)
+
+
 def flash_attention(
     q: torch.Tensor,
     k: torch.Tensor,

@@ -97,38 +97,55 @@ class TransformerLayer(TransformerLayerBaseIO):
                 return drop(x)
         return drop(x)
 
-    def attention_block(self, hidden_state: torch.Tensor, cumulative_seq_lengths: torch.Tensor, position_ids: torch.Tensor,
-                        use_cache: bool = False, reset_cache: bool = False, cache_index: int = 0,
-                        attention_scores_manipulation: Optional[torch.Tensor] = None,
-                        attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True) -> torch.Tensor:
+    def _attention_delta(self, hidden_state: torch.Tensor, cumulative_seq_lengths: torch.Tensor,
+                         position_ids: torch.Tensor, use_cache: bool, reset_cache: bool, cache_index: int,
+                         attention_scores_manipulation: Optional[torch.Tensor],
+                         attentions_score_manipulation_log_additive: Union[bool, list[bool]]) -> torch.Tensor:
         h = self.input_layernorm(hidden_state)
-        h = self.self_attention(
+        return self.self_attention(
             h, cumulative_seq_lengths=cumulative_seq_lengths, position_ids=position_ids, use_cache=use_cache,
             reset_cache=reset_cache, cache_index=cache_index, attention_scores_manipulation=attention_scores_manipulation,
             attentions_score_manipulation_log_additive=attentions_score_manipulation_log_additive,
         )
+
+    def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor) -> torch.Tensor:
+        out = residual + self._dropout(self.dropout_mlp, self.mlp(normed))
+        if hasattr(self, "mlp_adapter_name"):
+            out = out + self.apply_adapter(out, self.mlp_adapter_name)
+        return out
+
+    def attention_block(self, hidden_state: torch.Tensor, cumulative_seq_lengths: torch.Tensor, position_ids: torch.Tensor,
+                        use_cache: bool = False, reset_cache: bool = False, cache_index: int = 0,
+                        attention_scores_manipulation: Optional[torch.Tensor] = None,
+                        attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True) -> torch.Tensor:
+        h = self._attention_delta(hidden_state, cumulative_seq_lengths, position_ids, use_cache, reset_cache, cache_index,
+                                  attention_scores_manipulation, attentions_score_manipulation_log_additive)
         out = hidden_state + self._dropout(self.dropout_attention, h)
         if hasattr(self, "attn_adapter_name"):
             out = out + self.apply_adapter(out, self.attn_adapter_name)
         return out
 
     def mlp_block(self, hidden_state: torch.Tensor) -> torch.Tensor:
-        h = self.mlp(self.post_attention_layernorm(hidden_state))
-        out = hidden_state + self._dropout(self.dropout_mlp, h)
-        if hasattr(self, "mlp_adapter_name"):
-            out = out + self.apply_adapter(out, self.mlp_adapter_name)
-        return out
+        return self._mlp_tail(hidden_state, self.post_attention_layernorm(hidden_state))
 
     def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
         st = x.inference_settings
         assert x.cumulative_seq_lengths is not None
-        act = self.attention_block(
-            x.activations, x.cumulative_seq_lengths, x.position_ids,
-            use_cache=st.use_cache if st else False, reset_cache=st.reset_cache if st else False,
-            cache_index=st.cache_index if st else 0, attention_scores_manipulation=x.attention_scores_manipulation,
-            attentions_score_manipulation_log_additive=st.control_log_additive_batch if st else True,
-        )
-        act = self.mlp_block(act)
+        attn_args = (x.activations, x.cumulative_seq_lengths, x.position_ids,
+                     st.use_cache if st else False, st.reset_cache if st else False, st.cache_index if st else 0,
+                     x.attention_scores_manipulation, st.control_log_additive_batch if st else True)
+        if (self.dropout_attention.p == 0.0 or not self.training) and not hasattr(self, "attn_adapter_name"):
+            # residual stream through the fused norms: input_layernorm folds the residual-branch gradient into its
+            # backward; post_attention_layernorm writes x + attn and norm(x + attn) in one pass
+            resid, normed = self.input_layernorm.forward_add(x.activations, None)
+            h = self.self_attention(
+                normed, cumulative_seq_lengths=attn_args[1], position_ids=attn_args[2], use_cache=attn_args[3],
+                reset_cache=attn_args[4], cache_index=attn_args[5], attention_scores_manipulation=attn_args[6],
+                attentions_score_manipulation_log_additive=attn_args[7])
+            resid, normed = self.post_attention_layernorm.forward_add(resid, h)
+            act = self._mlp_tail(resid, normed)
+        else:
+            act = self.mlp_block(self.attention_block(*attn_args))
         if st is not None and (self.layer_index + 1) in st.embedding_layers:
             assert x.embeddings is not None
             x.embeddings[st.embedding_layers.index(self.layer_index + 1)] = act

@@ -58,6 +58,87 @@ def test_layer_norm(dtype):
     torch.testing.assert_close(b.grad.float(), br.grad, atol=tol * 20, rtol=tol * 2)
 
 
+@pytest.mark.parametrize("layer", [False, True])
+@pytest.mark.parametrize("dtype,rows", [(torch.bfloat16, 8192), (torch.float32, 300)])
+def test_add_norm_fused(layer, dtype, rows):
+    """s = x + r; y = norm(s): both outputs feed the loss so the fused residual-gradient add is exercised."""
+    torch.manual_seed(1)
+    H = 4096 if rows > 1000 else 512
+    x = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
+    r = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device=DEV, dtype=dtype)).requires_grad_(True)
+    if layer:
+        s, y = norm.add_layer_norm(x, r, w, b, 1e-5)
+    else:
+        s, y = norm.add_rms_norm(x, r, w, 1e-5)
+    xr, rr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, r, w, b))
+    sr = (xr + rr).to(dtype).float()  # the unfused path rounds the add to the activation dtype
+    sr = xr + rr + (sr - (xr + rr)).detach()
+    yr = (torch.nn.functional.layer_norm(sr, (H,), wr, br, 1e-5) if layer else norm.rms_norm_reference(sr, wr, 1e-5))
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(s.float(), sr, atol=0, rtol=0)
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    gs, gy = torch.randn_like(s), torch.randn_like(y)
+    torch.autograd.backward([s, y], [gs, gy])
+    torch.autograd.backward([sr, yr], [gs.float(), gy.float()])
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 3, rtol=tol * 2)
+    torch.testing.assert_close(r.grad.float(), rr.grad, atol=tol * 3, rtol=tol * 2)
+    wt = tol * (50 if rows > 1000 else 20)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=wt, rtol=tol * 2)
+    if layer:
+        torch.testing.assert_close(b.grad.float(), br.grad, atol=wt, rtol=tol * 2)
+    # dgamma reduction is deterministic (fixed-order two-level column sum)
+    dw0 = w.grad.clone()
+    w.grad = None
+    s, y = norm.add_layer_norm(x, r, w, b, 1e-5) if layer else norm.add_rms_norm(x, r, w, 1e-5)
+    torch.autograd.backward([s, y], [gs, gy])
+    assert torch.equal(dw0, w.grad)
+
+
+def test_norm_passthrough_and_layer_fusion():
+    """res=None: s aliases x and the gradient through s is added in the norm backward; the transformer layer's
+    fused residual path matches its unfused attention_block/mlp_block composition."""
+    torch.manual_seed(2)
+    H = 1024
+    x0 = torch.randn(64, H, device=DEV, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).requires_grad_(True)
+    x = x0 * 1.5
+    s, y = norm.add_rms_norm(x, None, w, 1e-5)
+    ((s * s).sum() + (y * y.flip(0)).sum()).backward()
+    xr = (x0.detach() * 1.5).requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    yr = norm.rms_norm_reference(xr, wr, 1e-5)
+    ((xr * xr).sum() + (yr * yr.flip(0)).sum()).backward()
+    torch.testing.assert_close(x0.grad, xr.grad * 1.5, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(w.grad, wr.grad, atol=1e-3, rtol=1e-4)
+
+    from scaling_amd.models import llama_architecture
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+    from scaling_amd.transformer.model.layers.base import TransformerLayerIO
+    from scaling_amd.transformer.model.layers.layer import TransformerLayer
+
+    arch = TransformerArchitectureConfig.from_dict(llama_architecture("llama_tiny", sequence_length=128))
+    layer = TransformerLayer(arch, layer_index=0).to(DEV)
+    seqs, T = 2, 128
+    a = torch.randn(seqs, T, arch.hidden_size, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cu = torch.arange(0, (seqs + 1) * T, T, device=DEV, dtype=torch.int32)
+    pos = torch.arange(T, device=DEV).repeat(seqs, 1)
+    out = layer(TransformerLayerIO(activations=a, position_ids=pos, cumulative_seq_lengths_padded=cu,
+                                   cumulative_seq_lengths=cu)).activations
+    g = torch.randn_like(out)
+    out.backward(g)
+    ga, gw = a.grad.clone(), [p.grad.clone() for p in layer.parameters()]
+    a.grad = None
+    layer.zero_grad()
+    ref = layer.mlp_block(layer.attention_block(a, cu, pos))
+    ref.backward(g)
+    torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(ga.float(), a.grad.float(), atol=5e-2, rtol=5e-2)
+    for p1, p2 in zip(gw, layer.parameters()):
+        torch.testing.assert_close(p1.float(), p2.grad.float(), atol=5e-1, rtol=5e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_swiglu_fused(dtype):
     torch.manual_seed(0)
@@ -74,7 +155,7 @@ def test_swiglu_fused(dtype):
 
 
 @pytest.mark.parametrize("interleaved", [False, True])
-@pytest.mark.parametrize("rot_frac", [1.0, 0.5])
+@pytest.mark.parametrize("rot_frac", [1.0, 0.5, 0.3125])  # 0.3125 -> rd 20: scalar fallback kernel
 def test_rope(interleaved, rot_frac):
     torch.manual_seed(0)
     T, nh, hd = 96, 6, 64
@@ -95,6 +176,59 @@ def test_rope(interleaved, rot_frac):
     y2 = rope.apply_rope(x.detach(), cos, sin, None, rd, 48, interleaved)
     y2r = rope.rope_reference(x.detach().float(), cos, sin, None, rd, 48, interleaved)
     torch.testing.assert_close(y2.float(), y2r, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+def test_rope_strided_and_inplace_out(interleaved):
+    torch.manual_seed(0)
+    T, nh, hd = 80, 4, 128
+    cos, sin = rope.rope_tables(hd, 256, 10000, interleaved, torch.bfloat16, DEV)
+    pos = torch.randint(0, 256, (T,), device=DEV)
+    x = torch.randn(T, nh, hd, device=DEV, dtype=torch.bfloat16)
+    ref = ext().rope(x, cos, sin, pos, hd, 64, interleaved, False)
+    buf = torch.zeros(T, 2 * nh * hd, device=DEV, dtype=torch.bfloat16)
+    out = buf[:, nh * hd:].view(T, nh, hd)
+    ext().rope(x, cos, sin, pos, hd, 64, interleaved, False, out)
+    assert torch.equal(out, ref) and torch.count_nonzero(buf[:, : nh * hd]) == 0
+    ext().rope(out, cos, sin, pos, hd, 64, interleaved, True, out)  # in place inverse
+    torch.testing.assert_close(out.float(), x.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("qkv_in_one", [False, True])
+def test_rope_flash_attention_fused(qkv_in_one):
+    """Fused rope+attention node == rope then flash attention, including the gradient of the QKV buffer."""
+    torch.manual_seed(3)
+    seqs, S, nq, nkv, hd = 2, 256, 8, 2, 128
+    if qkv_in_one:
+        nkv = nq
+    T = seqs * S
+    base = torch.randn(T, (nq + 2 * nkv) * hd, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+
+    def views(b):
+        if qkv_in_one:
+            qkv = b.view(T, nq, 3 * hd)
+            return qkv[..., :hd], qkv[..., hd:2 * hd], qkv[..., 2 * hd:]
+        return (b[:, : nq * hd].view(T, nq, hd), b[:, nq * hd:(nq + nkv) * hd].view(T, nkv, hd),
+                b[:, (nq + nkv) * hd:].view(T, nkv, hd))
+
+    cos, sin = rope.rope_tables(hd, S, 10000, False, torch.bfloat16, DEV)
+    pos = torch.arange(S, device=DEV).repeat(seqs)
+    cu = torch.arange(0, T + 1, S, device=DEV, dtype=torch.int32)
+    scale = hd ** -0.5
+    q, k, v = views(base)
+    o = attention.rope_flash_attention(base, q, k, v, cos, sin, pos, hd, S, False, cu, S, scale, True)
+    assert o is not None
+    g = torch.randn_like(o)
+    o.backward(g)
+    gf = base.grad.clone()
+    base.grad = None
+    q, k, v = views(base)
+    qr = rope.apply_rope(q, cos, sin, pos, hd, S, False)
+    kr = rope.apply_rope(k, cos, sin, pos, hd, S, False)
+    o2 = attention.flash_attention(qr, kr, v, cu, max_seqlen_q=S, softmax_scale=scale, causal=True)
+    o2.backward(g)
+    assert torch.equal(o, o2)
+    torch.testing.assert_close(gf.float(), base.grad.float(), atol=1e-2, rtol=1e-2)
 
 
 @pytest.mark.parametrize("V", [1000, 32000])
