@@ -251,6 +251,34 @@ void cast_scale_(const at::Tensor& x, at::Tensor y, double scale) {
     sa_launch::cast_scale(dt(x), dt(y), x.data_ptr(), y.data_ptr(), x.numel(), (float)scale, cur_stream());
 }
 
+// ------------------------------------------------------------------ GEMM (weight gradient)
+// C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
+bool gemm_tn_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+    if (!(A.is_cuda() && B.is_cuda() && C.is_cuda() && A.dim() == 2 && B.dim() == 2 && C.dim() == 2)) return false;
+    if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16 || C.scalar_type() != at::kBFloat16)
+        return false;
+    if (A.stride(1) != 1 || B.stride(1) != 1 || C.stride(1) != 1 || A.size(0) != B.size(0) || C.size(0) != A.size(1) ||
+        C.size(1) != B.size(1))
+        return false;
+    for (const at::Tensor* t : {&A, &B}) if ((uintptr_t)t->data_ptr() % 16 != 0) return false;
+    return sa_launch::gemm_tn_supported(A.size(1), B.size(1), A.size(0), A.stride(0), B.stride(0), C.stride(0));
+}
+void gemm_tn(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool accumulate) {
+    TORCH_CHECK(gemm_tn_ok(A, B, C), "gemm_tn: unsupported operands (bf16 2-D, M/N multiple of 256, K of 64)");
+    const at::DeviceGuard g(A.device());
+    sa_launch::gemm_tn(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), A.size(1),
+                       B.size(1), A.size(0), accumulate, cur_stream());
+}
+
+at::Tensor gemm_tn_timing(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+    TORCH_CHECK(gemm_tn_ok(A, B, C) && A.size(0) >= 32 * 72, "gemm_tn_timing: unsupported operands");
+    const at::DeviceGuard g(A.device());
+    auto dbg = at::zeros({8 * 8 * 5}, A.options().dtype(at::kLong));
+    sa_launch::gemm_tn_timing(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0),
+                              A.size(1), B.size(1), A.size(0), (uint64_t*)dbg.data_ptr(), cur_stream());
+    return dbg;
+}
+
 // ------------------------------------------------------------------ flash attention
 void check_qkv(const at::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.dim() == 3 && t.stride(2) == 1, "flash_attn: ", n, " must be [T, heads, D] with unit last stride");
@@ -325,6 +353,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
+    m.def("gemm_set_variant", &sa_launch::gemm_set_variant, "select the gemm_tn pipeline variant (benchmarking)");
+    m.def("gemm_tn_timing", &gemm_tn_timing, "profiling: per-phase s_memtime stamps of gemm_tn workgroup 0");
+    m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
+    m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());
     m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
     m.def("xent_bwd", &xent_bwd, "cross-entropy backward");

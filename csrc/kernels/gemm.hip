@@ -1,0 +1,420 @@
+// bf16 GEMM for the weight gradient of a linear layer on gfx950:  C[M, N] (+)= A^T B  with
+// A: [K, M] and B: [K, N] both stored k-major (row = reduction index), i.e. dW = dY^T X over the
+// token dimension.  hipBLASLt runs this "TN with both operands k-strided" shape at ~1.0 PF in the
+// 7B model (vs ~1.5 PF for the forward); here both operands are staged exactly as they lie in
+// memory and the MFMA fragments are produced by the hardware transposing LDS read.
+//
+//  * 256x256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), 128x64 per wave = 4x2 MFMA
+//    32x32x16 tiles (128 fp32 accumulators per lane).
+//  * K-tiles of 64 rows: A and B images [64][256] bf16 (512-B rows) filled by LDS-DMA
+//    (buffer_load ... lds, 16 B per lane, source-permuted so the lane-linear destination IS the
+//    swizzled image), two stages, the load of K-tile t+1 in flight while t is multiplied.
+//  * Image swizzle: 16-B slot index XOR ((row & 3) << 2) puts the four rows of every
+//    ds_read_b64_tr_b16 lane group in four different 64-B bank windows (conflict-free).
+//  * Operand fragments: ds_read_b64_tr_b16 pairs (k rows kb+4h..+3 and kb+8+4h..+3) give each lane 8
+//    k-values of its column; A and B use the same k permutation, so the MFMA sum is exact.
+//  * Grid: XCD-aware bijective remap, then 8-row groups of tiles so the 32 tiles resident on one XCD
+//    cover an 8x4 block and share A/B panels in its L2.
+//  * Epilogue: C = acc (+ C) with one bf16 rounding (beta = 1 accumulates into a main-grad buffer).
+#include "common.h"
+#include "flash_attn.h"
+#include "launch.h"
+
+using namespace sa;
+
+namespace sa_gemm {
+
+using fa::bf16x8;
+using fa::lds_s16x4;
+using fa::lds_void;
+
+constexpr int kWaves = 8;
+constexpr int kGroupM = 8;
+
+__device__ __forceinline__ int koff(int r, int c) {
+    return r * 512 + 16 * ((c >> 3) ^ ((r & 3) << 2)) + ((c & 7) << 1);
+}
+
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int kb, int c0, int lane) {
+    const int h = lane >> 5, g = (lane >> 4) & 1, i = lane & 15;
+    const int row = kb + 4 * h + (i >> 2);
+    const int col = c0 + 16 * g + 4 * (i & 3);
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + koff(row, col)));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + koff(row + 8, col)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int BK>
+struct Cfg {
+    static constexpr int kImg = BK * 256 * 2;           // one operand's K-tile image [BK][256] bf16
+    static constexpr int kStage = 2 * kImg;             // A + B
+    static constexpr int kPieces = kImg / 1024 / kWaves;  // LDS-DMA instructions per wave per image
+};
+
+// this wave's LDS-DMA pieces of one [BK][256] operand image: per-lane byte offsets relative to the K-tile's
+// first element (source-permuted swizzle), issued with the tile offset as the scalar soffset
+template <int NP, int NW = kWaves>
+struct Dma {
+    int voff[NP];
+    __device__ __forceinline__ void init(int wave, int lane, int ld) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int piece = wave + NW * i;
+            const int row = 2 * piece + (lane >> 5);
+            const int slot = (lane & 31) ^ ((row & 3) << 2);
+            voff[i] = (row * ld + slot * 8) * 2;
+        }
+    }
+    // Issued as inline asm on purpose: for a compiler-visible LDS-DMA the waitcnt pass cannot tell which LDS
+    // bytes are pending and puts s_waitcnt vmcnt(0) in front of every later ds_read, draining the whole
+    // prefetch pipeline each phase.  The kernel counts these loads itself (wait_vm) and retires them all
+    // before the epilogue.
+    // one piece (i must be a compile-time constant after unrolling)
+    __device__ __forceinline__ void load_piece(int i, const void* base, uint32_t nbytes, int soff, char* img,
+                                               int wave_u) const {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const uint64_t a = reinterpret_cast<uint64_t>(base);
+        const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
+                          (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffff),
+                          (int)__builtin_amdgcn_readfirstlane(nbytes), fa::kBufFlags};
+        const uint32_t lds = __builtin_amdgcn_readfirstlane(
+            (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)(img + (wave_u + NW * i) * 1024)));
+        int saved;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %1\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(saved)
+            : "s"(lds), "v"(voff[i]), "s"(rs), "s"(soff)
+            : "memory");
+    }
+    __device__ __forceinline__ void load(const void* base, uint32_t nbytes, int soff, char* img, int wave_u) const {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const uint64_t a = reinterpret_cast<uint64_t>(base);
+        const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
+                          (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffff),
+                          (int)__builtin_amdgcn_readfirstlane(nbytes), fa::kBufFlags};
+        const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+            (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)(img + wave_u * 1024)));
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+        {
+            int saved;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %1\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(saved)
+                : "s"(lds0 + i * NW * 1024), "v"(voff[i]), "s"(rs), "s"(soff)
+                : "memory");
+        }
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier that neither the compiler's memory ordering nor its scheduler moves anything across
+__device__ __forceinline__ void hard_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Ping-pong schedule.  Waves 0-3 (group 0) and 4-7 (group 1) share the four SIMDs pairwise.  Each K-tile of BK
+// rows is one phase per group:
+//     [fragment reads of the tile, LDS-DMA of tile t+LEAD, lgkmcnt(0)]  barrier  [MFMAs, vmcnt: tile t+1 landed]  barrier
+// Group 1 runs one barrier behind group 0, so on every SIMD one wave multiplies while its partner reads and stages.
+// Reads are retired before the first barrier, so a buffer can be restaged in the phase after its last read
+// (LEAD = STAGES - 1).  Tile t+1 must be retired by every wave before barrier event 2t+2, where group 0 starts
+// reading it: that is group 0's second barrier of phase t (LATEWAIT: its wait sits behind its MFMAs) but group
+// 1's FIRST barrier.  With two stages (LEAD 1) group 1 could not overlap its own DMA at all, so group 0 stages
+// every piece (DMA0) and group 1 never waits.
+constexpr int kDbgTiles = 8, kDbgT0 = 32, kDbgEv = 5;
+template <bool BETA, int BK, int STAGES, bool LATEWAIT, bool TIMING = false>
+__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                         const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                         u16* __restrict__ C, int ldc, int M, int N, int K,
+                                                         uint64_t* __restrict__ dbg = nullptr) {
+    using G = Cfg<BK>;
+    constexpr int KS = BK / 16;                   // MFMA k-steps per K-tile
+    constexpr bool SPLIT = STAGES == 2;           // group 0 stages A images, group 1 stages B images
+    constexpr int NW = SPLIT ? kWaves / 2 : kWaves;  // waves staging one image
+    constexpr int NP = G::kImg / 1024 / NW;       // LDS-DMA instructions per staging wave per operand image
+    constexpr int PT = SPLIT ? NP : 2 * NP;       // ... per K-tile
+    constexpr int LEAD = STAGES - 1;              // K-tiles in flight ahead of the one being read
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 2, wn = wave & 3;  // wm doubles as the ping-pong group
+
+    // tile coordinates
+    const int tm = M / 256, tn = N / 256, nwg = tm * tn;
+    const int v = xcd_remap(blockIdx.x, nwg);
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    Dma<NP, NW> da, db;
+    const bool stager = true;
+    const int swave = SPLIT ? wave & 3 : wave;
+    da.init(swave, lane, lda);
+    db.init(swave, lane, ldb);
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = K / BK;
+#define SA_ISSUE(t_)                                                                                      \
+    if (stager) {                                                                                         \
+        char* st_ = smem + ((t_) % STAGES) * G::kStage;                                                   \
+        const int k0_ = (t_) * BK;                                                                        \
+        da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave);          \
+        db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave); \
+    }
+    // retire tile `need` given that tiles up to `last` have been issued
+#define SA_RETIRE(need_, last_)                                                                           \
+    if (stager) {                                                                                         \
+        const int after_ = (last_) - (need_);                                                             \
+        if (after_ >= 3) wait_vm<PT * 3>();                                                               \
+        else if (after_ == 2) wait_vm<PT * 2>();                                                          \
+        else if (after_ == 1) wait_vm<PT>();                                                              \
+        else wait_vm<0>();                                                                                \
+    }
+    if constexpr (SPLIT) {
+        // Two stages.  Group 0 stages tile t+1's A image at the start of its read window of phase t and retires
+        // it behind its MFMAs (before barrier event 2t+2); group 1 stages tile t+2's B image inside its MFMA
+        // window of phase t (event 2t+2 onward: both groups' reads of tile t are retired by then) and retires it
+        // in its read window of phase t+1 (before event 2t+4).  Each wave has at most one image in flight.
+#define SA_ISSUE_G(t_)                                                                                    \
+        {                                                                                                 \
+            char* st_ = smem + ((t_) & 1) * G::kStage;                                                    \
+            const int k0_ = (t_) * BK;                                                                    \
+            if (wm == 0) da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave); \
+            else db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave); \
+        }
+        SA_ISSUE_G(0)
+        if (wm == 1 && nk > 1) {
+            SA_ISSUE_G(1)
+            wait_vm<NP>();
+        } else {
+            wait_vm<0>();
+        }
+        hard_barrier();
+        if (wm == 1) hard_barrier();
+        for (int t = 0; t < nk; ++t) {
+            const char* ia = smem + (t & 1) * G::kStage;
+            const char* ib = ia + G::kImg;
+            uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + STAGES * G::kStage) +
+                              (wave * kDbgTiles + (t - kDbgT0)) * kDbgEv;
+            const bool rec = TIMING && blockIdx.x == 0 && t >= kDbgT0 && t < kDbgT0 + kDbgTiles && lane == 0;
+#define SA_STAMP(e_) \
+            if (rec) stamp[e_] = __builtin_amdgcn_s_memtime();
+            SA_STAMP(0)
+            bf16x8 a[KS][4], b[KS][2];
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[ks][i] = frag_tr(ia, 16 * ks, 128 * wm + 32 * i, lane);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) b[ks][j] = frag_tr(ib, 16 * ks, 64 * wn + 32 * j, lane);
+            }
+            if (t + 1 < nk) {
+                if (wm == 0) SA_ISSUE_G(t + 1)
+                else wait_vm<0>();
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            SA_STAMP(1)
+            hard_barrier();
+            SA_STAMP(2)
+            __builtin_amdgcn_s_setprio(1);
+            // group 1 threads its B-image pieces for tile t+2 between the MFMAs (one per 32 / NP MFMAs) so
+            // they issue in the matrix pipe's shadow
+            const bool stage_b = wm == 1 && t + 2 < nk;
+            const int soff_b = __builtin_amdgcn_readfirstlane(((t + 2) * BK * ldb + n0) * 2);
+            char* st_b = smem + (t & 1) * G::kStage + G::kImg;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        acc[i][j] = fa::mfma(b[ks][j], a[ks][i], acc[i][j]);
+                        constexpr int every = (KS * 8) / NP;
+                        const int m = ks * 8 + i * 2 + j;
+                        if (m % every == every - 1 && stage_b) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            db.load_piece(m / every, B, b_bytes, soff_b, st_b, swave);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+            }
+            __builtin_amdgcn_s_setprio(0);
+            if (wm == 0 && t + 1 < nk) wait_vm<0>();
+            SA_STAMP(3)
+            hard_barrier();
+            SA_STAMP(4)
+        }
+#undef SA_STAMP
+#undef SA_ISSUE_G
+    } else {
+    // prologue: LEAD K-tiles in flight, tile 0 retired, group 1 one barrier behind
+#pragma unroll
+    for (int t = 0; t < LEAD; ++t)
+        if (t < nk) SA_ISSUE(t)
+    SA_RETIRE(0, min(LEAD, nk) - 1)
+    hard_barrier();
+    if (wm == 1) hard_barrier();
+    for (int t = 0; t < nk; ++t) {
+        const char* ia = smem + (t % STAGES) * G::kStage;
+        const char* ib = ia + G::kImg;
+        uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + STAGES * G::kStage) +
+                          (wave * kDbgTiles + (t - kDbgT0)) * kDbgEv;
+        const bool rec = TIMING && blockIdx.x == 0 && t >= kDbgT0 && t < kDbgT0 + kDbgTiles && lane == 0;
+#define SA_STAMP(e_) \
+        if (rec) stamp[e_] = __builtin_amdgcn_s_memtime();
+        SA_STAMP(0)
+        bf16x8 a[KS][4], b[KS][2];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[ks][i] = frag_tr(ia, 16 * ks, 128 * wm + 32 * i, lane);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[ks][j] = frag_tr(ib, 16 * ks, 64 * wn + 32 * j, lane);
+        }
+        const int last = min(t + LEAD, nk - 1);  // last tile issued once this phase has staged
+        if (t + LEAD < nk) SA_ISSUE(t + LEAD)
+        if ((!LATEWAIT || wm == 1) && t + 1 < nk) SA_RETIRE(t + 1, last)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        SA_STAMP(1)
+        hard_barrier();
+        SA_STAMP(2)
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = fa::mfma(b[ks][j], a[ks][i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (LATEWAIT && wm == 0 && t + 1 < nk) SA_RETIRE(t + 1, last)
+        SA_STAMP(3)
+        hard_barrier();
+        SA_STAMP(4)
+    }
+#undef SA_STAMP
+    }
+#undef SA_RETIRE
+#undef SA_ISSUE
+    if (wm == 0) hard_barrier();  // equal barrier counts for both groups
+    if (TIMING && blockIdx.x == 0) {
+        __syncthreads();
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(smem + STAGES * G::kStage);
+        for (int i = threadIdx.x; i < kWaves * kDbgTiles * kDbgEv; i += blockDim.x) dbg[i] = src[i];
+    }
+
+    // epilogue: acc[i][j][4q + e] = C[m0 + 128wm + 32i + (lane & 31)][n0 + 64wn + 32j + 8q + 4h + e]
+    const int h = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 32 * i + c) * ldc + n0 + 64 * wn + 4 * h;
+        u16x4 old[2][4];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) old[j][q] = *reinterpret_cast<const u16x4*>(crow_p + 32 * j + 8 * q);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = acc[i][j][4 * q + e];
+                    if (BETA) x += bf2f(old[j][q][e]);
+                    o[e] = f2bf(x);
+                }
+                *reinterpret_cast<u16x4*>(crow_p + 32 * j + 8 * q) = o;
+            }
+    }
+}
+
+// explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
+// template (the build's stub check catches that)
+#define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
+    template __global__ void gemm_tn_kernel<BETA, BK, S, LW, TM>(const u16* __restrict__, int, uint32_t,            \
+                                                                 const u16* __restrict__, int, uint32_t,            \
+                                                                 u16* __restrict__, int, int, int, int,             \
+                                                                 uint64_t* __restrict__);
+#define SA_GEMM_INST2(BK, S, LW) SA_GEMM_INST(true, BK, S, LW, false) SA_GEMM_INST(false, BK, S, LW, false)
+SA_GEMM_INST2(32, 4, false) SA_GEMM_INST2(32, 4, true) SA_GEMM_INST2(64, 2, true) SA_GEMM_INST2(32, 5, true)
+SA_GEMM_INST(false, 32, 4, true, true) SA_GEMM_INST(false, 64, 2, true, true)
+#undef SA_GEMM_INST2
+#undef SA_GEMM_INST
+
+template <bool BETA, int BK, int STAGES, bool LW>
+void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+               int64_t K, hipStream_t st) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+    hipLaunchKernelGGL((gemm_tn_kernel<BETA, BK, STAGES, LW>), dim3(nwg), dim3(512), STAGES * Cfg<BK>::kStage, st,
+                       (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
+                       (int)K, nullptr);
+}
+
+}  // namespace sa_gemm
+using namespace sa_gemm;
+
+namespace sa_launch {
+// pipeline variants (benchmarking hook): 2 (default) = BK 64 x 2 stages, split staging (one 32-MFMA block per
+// phase); 0 = BK 32 x 4 stages, wait behind the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages
+static int g_gemm_variant = 2;
+void gemm_set_variant(int v) { g_gemm_variant = v; }
+// profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
+void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+                    int64_t K, uint64_t* dbg, hipStream_t st) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+    const int extra = kWaves * kDbgTiles * kDbgEv * 8;
+    if (g_gemm_variant == 2)
+        hipLaunchKernelGGL((gemm_tn_kernel<false, 64, 2, true, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra,
+                           st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M,
+                           (int)N, (int)K, dbg);
+    else
+        hipLaunchKernelGGL((gemm_tn_kernel<false, 32, 4, true, true>), dim3(nwg), dim3(512), 4 * Cfg<32>::kStage + extra,
+                           st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M,
+                           (int)N, (int)K, dbg);
+}
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+    return M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 &&
+           ldb % 8 == 0 && ldc % 4 == 0 && K * lda * 2 < (int64_t(1) << 31) && K * ldb * 2 < (int64_t(1) << 31) &&
+           ldc < (1 << 30);
+}
+void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, bool beta, hipStream_t st) {
+#define SA_TN(BK, S, LW)                                                                      \
+    if (beta) launch_tn<true, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);                \
+    else launch_tn<false, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);
+    switch (g_gemm_variant) {
+        case 1: SA_TN(32, 4, false) break;
+        case 2: SA_TN(64, 2, true) break;
+        case 3: SA_TN(32, 5, true) break;
+        default: SA_TN(32, 4, true) break;
+    }
+#undef SA_TN
+}
+}  // namespace sa_launch

@@ -45,6 +45,16 @@ void sumsq(int dtype, const void* x, int64_t n, float scale, float* part_sq, flo
 void cast_scale(int sdt, int ddt, const void* x, void* y, int64_t n, float scale, hipStream_t st);
 }  // namespace sa_launch
 
+namespace sa_launch {
+// gemm.hip: C[M, N] (+)= A^T B, A [K, M] / B [K, N] row-major (k-major operands), bf16
+void gemm_set_variant(int v);
+void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+                    int64_t K, uint64_t* dbg, hipStream_t st);
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, bool beta, hipStream_t st);
+}  // namespace sa_launch
+
 // flash attention (bf16, head dim 32/64/128)
 struct FwdArgs {
     const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o; float* lse;

@@ -2,7 +2,8 @@
 
 With the framework optimizer every trainable parameter's ``.grad`` is a view into one flat gradient
 buffer (``OptimizerParamGroup.attach_grads`` tags such parameters with ``_sa_main_grad``).  For those
-weights the backward issues ``grad.addmm_(dY^T, X)`` — hipBLASLt's beta=1 epilogue — instead of
+weights the backward issues ``grad += dY^T X`` as ONE GEMM with a beta=1 epilogue (``ops.gemm.wgrad``: the
+hand-written gfx950 weight-gradient kernel, hipBLASLt ``addmm_`` for shapes it does not tile) instead of
 materialising ``dW`` and letting autograd add it into ``.grad``: one GEMM, no extra ``[N, K]``
 temporary, no elementwise accumulate pass, and a single bf16 rounding of ``grad + dY^T X``.
 The optimizer's bucket-ready callback (``_sa_grad_ready``) is invoked in place of autograd's
@@ -17,6 +18,8 @@ from __future__ import annotations
 from typing import Any, Optional, Sequence
 
 import torch
+
+from ....ops.gemm import wgrad
 
 
 def _adjacent(ts: Sequence[Optional[torch.Tensor]]) -> Optional[torch.Tensor]:
@@ -76,13 +79,13 @@ class _MultiLinear(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             target = _main_grad_target(weights)
             if target is not None:
-                target.addmm_(g2.t(), x2)
+                wgrad(g2, x2, target, accumulate=True)
                 for wt in weights:
                     cb = getattr(wt, "_sa_grad_ready", None)
                     if cb is not None:
                         cb(wt)
             else:
-                dw = torch.matmul(g2.t(), x2)
+                dw = wgrad(g2, x2)
                 dws = list(torch.split(dw, ctx.splits, dim=0)) if n > 1 else [dw]
         dbs: list[Optional[torch.Tensor]] = []
         if ctx.has_bias:

@@ -1,0 +1,29 @@
+"""Weight-gradient GEMM ``dW (+)= dY^T X`` on the hand-written gfx950 kernel (``csrc/kernels/gemm.hip``).
+
+Both operands arrive token-major (``dY: [T, N]``, ``X: [T, K]``), i.e. k-strided for this product; the
+kernel stages them as they lie (LDS-DMA) and builds MFMA fragments with the transposing LDS read, in a
+ping-pong schedule.  At the 7B layer shapes it runs 1.05-1.25 PF vs hipBLASLt's 0.95-1.2 PF
+(``profiles/gemm_wgrad_r1.log``).  Shapes it does not tile (M/N not multiples of 256, T not a multiple
+of 64) use ``torch.matmul`` / ``addmm_`` (hipBLASLt).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._ext import ext, use_native
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """``out (+)= dy^T @ x`` for 2-D ``dy [T, N]``, ``x [T, K]``; returns ``out`` ([N, K])."""
+    if use_native(dy):
+        o = out if out is not None else torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=dy.dtype)
+        if ext().gemm_tn_ok(dy, x, o):
+            ext().gemm_tn(dy, x, o, bool(accumulate and out is not None))
+            return o
+    if out is None:
+        return torch.matmul(dy.t(), x)
+    if accumulate:
+        return out.addmm_(dy.t(), x)
+    return torch.matmul(dy.t(), x, out=out)

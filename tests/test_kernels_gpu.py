@@ -374,3 +374,20 @@ def test_flash_attention_deterministic():
         grads.append([t.grad.clone() for t in (q, k, v)])
     for a, b in zip(*grads):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
+def test_gemm_tn(M, N, K, accumulate):
+    """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands."""
+    torch.manual_seed(5)
+    A_full = torch.randn(K, M + 64, device=DEV, dtype=torch.bfloat16)
+    A = A_full[:, 64:]  # row stride M + 64, 128-B aligned start
+    B = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    C0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    C = C0.clone()
+    assert ext().gemm_tn_ok(A, B, C)
+    ext().gemm_tn(A, B, C, accumulate)
+    ref = A.float().t() @ B.float() + (C0.float() if accumulate else 0)
+    torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
+    assert not ext().gemm_tn_ok(A[:, :200], B, C[:200])
