@@ -282,12 +282,20 @@ at::Tensor gemm_tn_timing(const at::Tensor& A, const at::Tensor& B, const at::Te
 // ------------------------------------------------------------------ flash attention
 void check_qkv(const at::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.dim() == 3 && t.stride(2) == 1, "flash_attn: ", n, " must be [T, heads, D] with unit last stride");
-    TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash_attn: ", n, " must be bfloat16");
+    TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, "flash_attn: ", n, " must be bfloat16 or float16");
     TORCH_CHECK(t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0, "flash_attn: ", n, " strides must be multiples of 8");
 }
+// dropout keep threshold on the 32-bit mix: P(keep) = 1 - p
+uint32_t drop_threshold(double p) {
+    const double t = p * 4294967296.0;
+    return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+}
 std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& cu_q,
-                               const at::Tensor& cu_k, int64_t max_q, double scale, bool causal, int64_t window) {
+                               const at::Tensor& cu_k, int64_t max_q, double scale, bool causal, int64_t window,
+                               double p_drop, int64_t seed) {
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
+    TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash_attn: q/k/v dtypes differ");
+    TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "flash_attn: dropout probability must be in [0, 1)");
     const int64_t D = q.size(2);
     TORCH_CHECK(D == 32 || D == 64 || D == 128, "flash_attn: head dim must be 32, 64 or 128");
     TORCH_CHECK(k.size(2) == D && v.size(2) == D && k.size(1) == v.size(1) && q.size(1) % k.size(1) == 0, "flash_attn: shapes");
@@ -304,16 +312,19 @@ std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const a
     a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
     a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)k.size(1); a.causal = causal ? 1 : 0; a.window = (int)window;
     a.scale_log2 = (float)(scale * 1.4426950408889634);
-    if (T > 0 && a.nseg > 0) sa_launch::fa_fwd(a, (int)D, (int)max_q, cur_stream());
+    a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
+    if (T > 0 && a.nseg > 0) sa_launch::fa_fwd(a, (int)D, (int)max_q, q.scalar_type() == at::kHalf, cur_stream());
     return {o, lse};
 }
 std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                                const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_q, const at::Tensor& cu_k,
                                int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window,
                                const c10::optional<at::Tensor>& dq_out, const c10::optional<at::Tensor>& dk_out,
-                               const c10::optional<at::Tensor>& dv_out) {
+                               const c10::optional<at::Tensor>& dv_out, double p_drop, int64_t seed) {
     // d*_out: write the gradients into caller-provided strided views (e.g. slices of one dQKV buffer)
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(o, "o");
+    TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() && o.scalar_type() == q.scalar_type() &&
+                dout.scalar_type() == q.scalar_type(), "fa_bwd: dtypes differ");
     auto dO = dout.contiguous();
     check_qkv(dO, "dout");
     const int64_t D = q.size(2), T = q.size(0), H = q.size(1), Tk = k.size(0), Hk = k.size(1);
@@ -340,10 +351,89 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
     a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
     a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)Hk; a.causal = causal ? 1 : 0; a.window = (int)window;
     a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
+    a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
     if (T > 0 && a.nseg > 0)
         sa_launch::fa_bwd(a, (const uint16_t*)o.data_ptr(), o.stride(0), o.stride(1), T, (int)D, (int)max_q, (int)max_k,
-                          cur_stream());
+                          q.scalar_type() == at::kHalf, cur_stream());
     return {dq, dk, dv};
+}
+// ------------------------------------------------------------------ masked softmax / activations / dropout
+at::Tensor aligned16(const at::Tensor& t) {
+    auto c = t.contiguous();
+    return (reinterpret_cast<uintptr_t>(c.data_ptr()) % 16 == 0) ? c : c.clone();
+}
+// mask: optional bool tensor broadcastable to x [B, H, Sq, Sk] with unit last stride
+std::tuple<const void*, int64_t, int64_t, int64_t> mask_view(const c10::optional<at::Tensor>& mask, const at::Tensor& x,
+                                                             at::Tensor& keep) {
+    if (!mask.has_value()) return {nullptr, 0, 0, 0};
+    TORCH_CHECK(mask->scalar_type() == at::kBool, "masked_softmax: mask must be bool");
+    auto m = mask->to(x.device()).expand(x.sizes());
+    if (m.stride(3) != 1) m = m.contiguous();
+    keep = m;
+    return {m.data_ptr(), m.stride(0), m.stride(1), m.stride(2)};
+}
+at::Tensor masked_softmax_fwd(const at::Tensor& x_, const c10::optional<at::Tensor>& mask, double scale, double fill,
+                              bool round_scaled) {
+    TORCH_CHECK(x_.is_cuda() && x_.dim() == 4, "masked_softmax: x must be a [B, H, Sq, Sk] GPU tensor");
+    const at::DeviceGuard g(x_.device());
+    auto x = aligned16(x_);
+    at::Tensor keep;
+    auto [mp, mb, mh, mq] = mask_view(mask, x, keep);
+    auto y = at::empty_like(x);
+    const int64_t N = x.size(3), rows = x.numel() / std::max<int64_t>(N, 1);
+    if (rows > 0 && N > 0)
+        sa_launch::masked_softmax_fwd(dt(x), x.data_ptr(), mp, y.data_ptr(), rows, (int)N, (int)x.size(1), (int)x.size(2), mb, mh,
+                                      mq, (float)scale, (float)fill, round_scaled, cur_stream());
+    return y;
+}
+at::Tensor masked_softmax_bwd(const at::Tensor& dy_, const at::Tensor& y_, const c10::optional<at::Tensor>& mask, double scale) {
+    TORCH_CHECK(y_.is_cuda() && y_.dim() == 4 && dy_.sizes() == y_.sizes() && dy_.scalar_type() == y_.scalar_type(),
+                "masked_softmax_bwd: shapes");
+    const at::DeviceGuard g(y_.device());
+    auto y = aligned16(y_);
+    auto dy = aligned16(dy_);
+    at::Tensor keep;
+    auto [mp, mb, mh, mq] = mask_view(mask, y, keep);
+    auto dx = at::empty_like(y);
+    const int64_t N = y.size(3), rows = y.numel() / std::max<int64_t>(N, 1);
+    if (rows > 0 && N > 0)
+        sa_launch::masked_softmax_bwd(dt(y), dy.data_ptr(), y.data_ptr(), mp, dx.data_ptr(), rows, (int)N, (int)y.size(1),
+                                      (int)y.size(2), mb, mh, mq, (float)scale, cur_stream());
+    return dx;
+}
+at::Tensor act_fwd(const at::Tensor& x_, int64_t kind) {
+    TORCH_CHECK(x_.is_cuda(), "activation: GPU tensor expected");
+    const at::DeviceGuard g(x_.device());
+    auto x = aligned16(x_);
+    auto y = at::empty_like(x);
+    if (x.numel() > 0) sa_launch::act_fwd(dt(x), x.data_ptr(), y.data_ptr(), x.numel(), (int)kind, cur_stream());
+    return y;
+}
+at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind) {
+    TORCH_CHECK(x_.is_cuda() && dy_.sizes() == x_.sizes() && dy_.scalar_type() == x_.scalar_type(), "activation_bwd: shapes");
+    const at::DeviceGuard g(x_.device());
+    auto x = aligned16(x_);
+    auto dy = aligned16(dy_);
+    auto dx = at::empty_like(x);
+    if (x.numel() > 0) sa_launch::act_bwd(dt(x), dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), (int)kind, cur_stream());
+    return dx;
+}
+// out = res + dropout(x); res optional (plain dropout).  Backward = dropout(g) with the same seed.
+at::Tensor dropout_add(const at::Tensor& x_, const c10::optional<at::Tensor>& res_, double p, int64_t seed) {
+    TORCH_CHECK(x_.is_cuda(), "dropout: GPU tensor expected");
+    TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: probability must be in [0, 1)");
+    const at::DeviceGuard g(x_.device());
+    auto x = aligned16(x_);
+    at::Tensor res;
+    if (res_.has_value()) {
+        TORCH_CHECK(res_->sizes() == x.sizes() && res_->scalar_type() == x.scalar_type(), "dropout_add: residual mismatch");
+        res = aligned16(*res_);
+    }
+    auto out = at::empty_like(x);
+    if (x.numel() > 0)
+        sa_launch::dropout(dt(x), x.data_ptr(), res.defined() ? res.data_ptr() : nullptr, out.data_ptr(), x.numel(),
+                           (uint32_t)seed, drop_threshold(p), (float)(1.0 / (1.0 - p)), cur_stream());
+    return out;
 }
 }  // namespace
 
@@ -365,6 +455,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("adamw_", &adamw_, "fused AdamW on flat fp32 buffers");
     m.def("sumsq_", &sumsq_, "sum of squares + non-finite count");
     m.def("cast_scale_", &cast_scale_, "y = cast(x * scale)");
-    m.def("fa_fwd", &fa_fwd, "flash attention forward");
-    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none());
+    m.def("masked_softmax_fwd", &masked_softmax_fwd, "softmax(masked_fill(x * scale, mask, fill)) over the last dim", py::arg("x"), py::arg("mask"), py::arg("scale"), py::arg("fill"), py::arg("round_scaled"));
+    m.def("masked_softmax_bwd", &masked_softmax_bwd, "masked softmax backward", py::arg("dy"), py::arg("y"), py::arg("mask"), py::arg("scale"));
+    m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
+    m.def("act_bwd", &act_bwd, "activation backward");
+    m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
+    m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0);
+    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0);
 }

@@ -160,6 +160,49 @@ __device__ __forceinline__ float sum_xchg32(float x) {
     xchg32(x, a, b);
     return a + b;
 }
+// ---- element type: bf16 or fp16 operands (same 16-bit layouts; MFMA variant + conversions differ)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <bool F16>
+__device__ __forceinline__ f32x16 mma(bf16x8 a, bf16x8 b, f32x16 c) {
+    if constexpr (F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool F16>
+__device__ __forceinline__ bf16x8 pack_acc_t(const f32x16& acc, int s) {
+    if constexpr (F16) {
+        f16x8 r;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = (_Float16)acc[8 * s + j];
+        return __builtin_bit_cast(bf16x8, r);
+    } else {
+        return pack_acc(acc, s);
+    }
+}
+template <bool F16>
+__device__ __forceinline__ u16 f2t(float f) {
+    if constexpr (F16) return __builtin_bit_cast(u16, (_Float16)f);
+    else return f2bf(f);
+}
+
+// ---- attention dropout: counter-based keep mask, a pure function of (seed, q head, query token, key
+// token), so the forward and both backward kernels (different lane <-> element layouts) regenerate the
+// identical mask without storing it.  mix32 is the "lowbias32" integer finaliser (bijective).
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ uint32_t drop_head(uint32_t seed, int head) { return mix32(seed ^ ((uint32_t)head * 0x9e3779b9u)); }
+__device__ __forceinline__ uint32_t drop_row(uint32_t hs, int qtok) { return mix32(hs + (uint32_t)qtok); }
+__device__ __forceinline__ bool drop_keep(uint32_t row, int ktok, uint32_t thr) {
+    return mix32(row ^ ((uint32_t)ktok * 0x85ebca6bu)) >= thr;
+}
+
 // row offset (r) of accumulator register j in a 32x32 MFMA C tile, excluding the 4h lane term
 __host__ __device__ constexpr int crow(int j) { return (j & 3) + 8 * (j >> 2); }
 

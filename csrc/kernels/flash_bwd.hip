@@ -14,9 +14,9 @@
 using namespace sa;
 using namespace sa::fa;
 
-template <int D>
-__global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const u16* __restrict__ o, int64_t o_tok, int64_t o_head,
-                                                         const u16* __restrict__ dO, int64_t d_tok, int64_t d_head,
+template <int D, typename E>
+__global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
+                                                         const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
                                                          float* __restrict__ delta, const float* __restrict__ lse,
                                                          float* __restrict__ lse2, int64_t T, int H) {
     constexpr int LPR = D / 8;  // lanes per row
@@ -31,8 +31,8 @@ __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const u16* __restrict__
         t = row / H;
         hh = (int)(row % H);
         float a[8], b[8];
-        V8<u16>::ld(o + t * o_tok + hh * o_head + 8 * c, a);
-        V8<u16>::ld(dO + t * d_tok + hh * d_head + 8 * c, b);
+        V8<E>::ld(o + t * o_tok + hh * o_head + 8 * c, a);
+        V8<E>::ld(dO + t * d_tok + hh * d_head + 8 * c, b);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += a[j] * b[j];
     }
@@ -81,8 +81,9 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const int (&t
 //   S = Q K^T, dP = dO V^T (row reads), p = exp2(S c - lse2), dS = p (dP - delta),
 //   dV^T += dO^T P, dK^T += Q^T dS (transposed reads; P / dS accumulators are the B operands).
 // Query rows past the segment arrive as zeros (Q = dO = 0, lse2 = delta = 0) and contribute nothing.
-template <int D>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, BUF = 2 * TILE + 512, NKS = D / 16, NT = D / 32;
     // grid (Hkv, nseg, key blocks): key block slowest so causal work is issued heaviest-first
@@ -147,6 +148,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
         const float* DL = LS + 64;
         const int qt = qlo + (w % ntq) * 64;
+        uint32_t hs = 0;
+        if constexpr (DROP) hs = drop_head(a.seed, hk * grp + w / ntq);
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
                                (a.window >= 0 && (kw0 < qt + 63 + off - a.window || (!a.causal && kw0 + 31 > qt + off + a.window)));
 #pragma unroll
@@ -154,8 +157,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
             f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                s = mfma(rd_row<D>(Q, 32 * b * D * 2, lo.row[ks]), rd_row<D>(kw_img, 0, lo.row[ks]), s);
-                dp = mfma(rd_row<D>(DO, 32 * b * D * 2, lo.row[ks]), rd_row<D>(vw_img, 0, lo.row[ks]), dp);
+                s = mma<F16>(rd_row<D>(Q, 32 * b * D * 2, lo.row[ks]), rd_row<D>(kw_img, 0, lo.row[ks]), s);
+                dp = mma<F16>(rd_row<D>(DO, 32 * b * D * 2, lo.row[ks]), rd_row<D>(vw_img, 0, lo.row[ks]), dp);
             }
 #pragma unroll
             for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
@@ -181,18 +184,25 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                     const int r = 4 * g + j;
                     float p = fast_exp2(__builtin_fmaf(s[r], c2, -l4[j]));
                     if (need_mask) p = (crow(r) >= mlo && crow(r) <= mhi) ? p : 0.f;
-                    s[r] = p;
-                    dp[r] = p * (dp[r] - d4[j]);
+                    if constexpr (DROP) {  // dV sees the dropped P; dS = P (Z dP / (1-p) - delta)
+                        const int qtok = q0s + qt + 32 * b + 4 * h + crow(r);
+                        const bool keep = drop_keep(drop_row(hs, qtok), k0s + mykey, a.drop_thr);
+                        s[r] = keep ? p * a.rp_drop : 0.f;
+                        dp[r] = p * ((keep ? dp[r] * a.rp_drop : 0.f) - d4[j]);
+                    } else {
+                        s[r] = p;
+                        dp[r] = p * (dp[r] - d4[j]);
+                    }
                 }
             }
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 pb = pack_acc(s, ss), db = pack_acc(dp, ss);
+                const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
                 const int kb = (32 * b + 16 * ss) * D * 2;
 #pragma unroll
                 for (int t = 0; t < NT; ++t) {
-                    dv[t] = mfma(rd_tr<D>(DO, kb, lo.tr[t]), pb, dv[t]);
-                    dk[t] = mfma(rd_tr<D>(Q, kb, lo.tr[t]), db, dk[t]);
+                    dv[t] = mma<F16>(rd_tr<D>(DO, kb, lo.tr[t]), pb, dv[t]);
+                    dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo.tr[t]), db, dk[t]);
                 }
             }
 #pragma unroll
@@ -228,20 +238,22 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 u16x4 wk, wv;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    wk[j] = f2bf(dk[t][4 * g + j] * a.scale);
-                    wv[j] = f2bf(dv[t][4 * g + j]);
+                    wk[j] = f2t<F16>(dk[t][4 * g + j] * a.scale);
+                    wv[j] = f2t<F16>(dv[t][4 * g + j]);
                 }
                 *reinterpret_cast<u16x4*>(kp + 32 * t + 8 * g + 4 * h) = wk;
                 *reinterpret_cast<u16x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
             }
     }
+#endif
 }
 
 // dQ: workgroup = 4 waves x 32 queries of one (segment, q head); query on the lane (Q, dO rows are
 // register-resident B operands), K / V tiles of 64 keys double-buffered in LDS by LDS-DMA.  Per 32-key block:
 //   S^T = K Q^T, dP^T = V dO^T, p = exp2(S c - lse2), dS = p (dP - delta), dQ^T += K^T dS^T.
-template <int D>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
     const int seg = blockIdx.y, hq = blockIdx.x;  // grid (Hq, nseg, q tiles), heaviest tiles first
@@ -276,6 +288,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     }
     const float nl2 = myq < Lq ? -a.lse[(int64_t)hq * a.lse_stride + q0s + myq] * 1.4426950408889634f : -INFINITY;
     const float dlt = myq < Lq ? a.delta[(int64_t)hq * a.lse_stride + q0s + myq] : 0.f;
+    uint32_t drow = 0;
+    if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
     LdsOffsets<D> lo;
     lo.init(lane);
     DmaTile<D, 4> tk, tv;
@@ -304,8 +318,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
             f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                s = mfma(rd_row<D>(K, 32 * b * D * 2, lo.row[ks]), qf[ks], s);
-                dp = mfma(rd_row<D>(V, 32 * b * D * 2, lo.row[ks]), df[ks], dp);
+                s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row[ks]), qf[ks], s);
+                dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row[ks]), df[ks], dp);
             }
             // key of register j: kt + 32b + 4h + crow(j)
             int hi = 1 << 30, low = -1 << 30;
@@ -320,14 +334,19 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
             for (int r = 0; r < 16; ++r) {
                 float p = fast_exp2(__builtin_fmaf(s[r], c2, nl2));
                 if (need_mask) p = (crow(r) <= hi && crow(r) >= low) ? p : 0.f;
-                dp[r] = p * (dp[r] - dlt);
+                if constexpr (DROP) {
+                    const bool keep = drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(r), a.drop_thr);
+                    dp[r] = p * ((keep ? dp[r] * a.rp_drop : 0.f) - dlt);
+                } else {
+                    dp[r] = p * (dp[r] - dlt);
+                }
             }
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 db = pack_acc(dp, ss);
+                const bf16x8 db = pack_acc_t<F16>(dp, ss);
                 const int kb = (32 * b + 16 * ss) * D * 2;
 #pragma unroll
-                for (int t = 0; t < NT; ++t) dq[t] = mfma(rd_tr<D>(K, kb, lo.tr[t]), db, dq[t]);
+                for (int t = 0; t < NT; ++t) dq[t] = mma<F16>(rd_tr<D>(K, kb, lo.tr[t]), db, dq[t]);
             }
         }
     };
@@ -356,35 +375,59 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
             for (int g = 0; g < 4; ++g) {
                 u16x4 w;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = f2bf(dq[t][4 * g + j] * a.scale);
+                for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(dq[t][4 * g + j] * a.scale);
                 *reinterpret_cast<u16x4*>(qp + 32 * t + 8 * g + 4 * h) = w;
             }
+    }
+#endif
+}
+
+template <bool F16, bool DROP>
+static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
+    {
+        dim3 grid(a.Hkv, a.nseg, (max_k + 127) / 128);
+        const size_t lds = 2 * (2 * 64 * D * 2 + 512) + 4 * 64 * D * 2;
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
+        else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
+    }
+    {
+        dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
+        const size_t lds = 4 * 64 * D * 2;
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
+        else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
+    }
+}
+
+template <int D, typename T>
+static void launch_bwd_dot(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, hipStream_t st) {
+    const int64_t threads = Tq * a.Hq * (D / 8);
+    const int grid = (int)((threads + 255) / 256);
+    hipLaunchKernelGGL((fa_bwd_dot_kernel<D, T>), grid, 256, 0, st, (const T*)o, o_tok, o_head, (const T*)a.dO, a.do_tok,
+                       a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
+}
+
+template <int D>
+static void launch_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int max_q,
+                       int max_k, bool f16, hipStream_t st) {
+    const bool drop = a.p_drop > 0.f;
+    if (f16) {
+        launch_bwd_dot<D, _Float16>(a, o, o_tok, o_head, Tq, st);
+        if (drop) launch_bwd_main<true, true>(a, D, max_q, max_k, st);
+        else launch_bwd_main<true, false>(a, D, max_q, max_k, st);
+    } else {
+        launch_bwd_dot<D, u16>(a, o, o_tok, o_head, Tq, st);
+        if (drop) launch_bwd_main<false, true>(a, D, max_q, max_k, st);
+        else launch_bwd_main<false, false>(a, D, max_q, max_k, st);
     }
 }
 
 namespace sa_launch {
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
-            hipStream_t st) {
-    {
-        const int64_t threads = Tq * a.Hq * (D / 8);
-        const int grid = (int)((threads + 255) / 256);
-        if (D == 128) hipLaunchKernelGGL(fa_bwd_dot_kernel<128>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
-        else if (D == 64) hipLaunchKernelGGL(fa_bwd_dot_kernel<64>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
-        else hipLaunchKernelGGL(fa_bwd_dot_kernel<32>, grid, 256, 0, st, o, o_tok, o_head, a.dO, a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
-    }
-    {
-        dim3 grid(a.Hkv, a.nseg, (max_k + 127) / 128);
-        const size_t lds = 2 * (2 * 64 * D * 2 + 512) + 4 * 64 * D * 2;
-        if (D == 128) hipLaunchKernelGGL(fa_bwd_dkdv_kernel<128>, grid, 256, lds, st, a);
-        else if (D == 64) hipLaunchKernelGGL(fa_bwd_dkdv_kernel<64>, grid, 256, lds, st, a);
-        else hipLaunchKernelGGL(fa_bwd_dkdv_kernel<32>, grid, 256, lds, st, a);
-    }
-    {
-        dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
-        const size_t lds = 4 * 64 * D * 2;
-        if (D == 128) hipLaunchKernelGGL(fa_bwd_dq_kernel<128>, grid, 256, lds, st, a);
-        else if (D == 64) hipLaunchKernelGGL(fa_bwd_dq_kernel<64>, grid, 256, lds, st, a);
-        else hipLaunchKernelGGL(fa_bwd_dq_kernel<32>, grid, 256, lds, st, a);
-    }
+            bool f16, hipStream_t st) {
+    if (D == 128) launch_bwd<128>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
+    else if (D == 64) launch_bwd<64>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
+    else launch_bwd<32>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
 }
 }  // namespace sa_launch

@@ -12,8 +12,9 @@
 using namespace sa;
 using namespace sa::fa;
 
-template <int D>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2;  // bytes per K or V tile
     // buffer b: K at smem + 2*b*TILE, V at smem + (2*b+1)*TILE
@@ -54,6 +55,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) o[t] = f32x16{};
     float m = -INFINITY, lsum = 0.f;
+    uint32_t drow = 0;
+    if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
 
     const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
 #pragma unroll
-            for (int b = 0; b < 2; ++b) s[b] = mfma(ld_row<D>(K, 32 * b + lq, 16 * ks + 8 * h), qf[ks], s[b]);
+            for (int b = 0; b < 2; ++b) s[b] = mma<F16>(ld_row<D>(K, 32 * b + lq, 16 * ks + 8 * h), qf[ks], s[b]);
         }
         // ---- scale + mask (mask only on boundary tiles; wave-uniform decision)
         const bool need_mask = (kt + 64 > Lk) || (a.causal && kt + 63 > qw0 + off) ||
@@ -117,6 +120,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
         rs += __shfl_xor(rs, 32, 64);
         lsum = lsum * alpha + rs;
         m = mnew;
+        if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (!drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(r), a.drop_thr)) s[b][r] = 0.f;
+        }
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
 #pragma unroll
@@ -126,13 +136,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc(s[b], ss);
+            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
 #pragma unroll
             for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int ss = 0; ss < 2; ++ss) o[t] = mfma(ld_tr<D>(V, 32 * b + 16 * ss, 32 * t), pf[b][ss], o[t]);
+                for (int ss = 0; ss < 2; ++ss) o[t] = mma<F16>(ld_tr<D>(V, 32 * b + 16 * ss, 32 * t), pf[b][ss], o[t]);
         if (has_next) {
             sk.store(smem + 2 * (cur ^ 1) * TILE);
             sv.store(smem + (2 * (cur ^ 1) + 1) * TILE);
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     }
     // ---- epilogue: O = O^T / l, lse = (m + log2 l) * ln2
     if (myq < Lq) {
-        const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+        const float inv = (lsum > 0.f ? 1.f / lsum : 0.f) * (DROP ? a.rp_drop : 1.f);
         u16* op = a.o + (int64_t)(q0s + myq) * a.o_tok + (int64_t)hq * a.o_head;
 #pragma unroll
         for (int t = 0; t < D / 32; ++t)
@@ -150,11 +160,12 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
             for (int g = 0; g < 4; ++g) {
                 u16x4 w;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = f2bf(o[t][4 * g + j] * inv);
+                for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(o[t][4 * g + j] * inv);
                 *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * h) = w;
             }
         if (h == 0) a.lse[(int64_t)hq * a.lse_stride + q0s + myq] = lsum > 0.f ? (m + __log2f(lsum)) * 0.69314718055994530942f : INFINITY;
     }
+#endif
 }
 
 
@@ -175,8 +186,9 @@ struct FwdV2 {
     static constexpr float TH = 8.f;
 };
 
-template <int D>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     using C = FwdV2<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
@@ -237,6 +249,8 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
     for (int t = 0; t < C::NT; ++t) o[t] = f32x16{};
     float m = -INFINITY, l = 0.f;
     const float c2 = a.scale_log2;
+    uint32_t drow = 0;
+    if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
 
     auto tile = [&](const char* K, int kt) {
         const char* V = K + C::TILE;
@@ -245,7 +259,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
         for (int ks = 0; ks < C::NKS; ++ks)
 #pragma unroll
             for (int b = 0; b < 2; ++b)
-                s[b] = mfma(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
+                s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
         // keep the K fragment reads one or two MFMAs ahead instead of hoisting all of them
 #pragma unroll
         for (int i = 0; i < 2 * C::NKS; ++i) {
@@ -297,11 +311,18 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
                 rs += p;
             }
         l += sum_xchg32(rs);
+        if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (!drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(j), a.drop_thr)) s[b][j] = 0.f;
+        }
         bf16x8 pf[2][2];
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc(s[b], ss);
+            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
 #pragma unroll
         for (int t = 0; t < C::NT; ++t)
 #pragma unroll
@@ -311,7 +332,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
                     const int kb = (32 * b + 16 * ss) * D * 2;
                     const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
                     const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
-                    o[t] = mfma(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
+                    o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
                 }
 #pragma unroll
         for (int i = 0; i < 4 * C::NT; ++i) {
@@ -338,7 +359,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_FWD_ISSUE
     if (myq < Lq) {
-        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const float inv = (l > 0.f ? 1.f / l : 0.f) * (DROP ? a.rp_drop : 1.f);
         u16* op = a.o + (int64_t)(q0s + myq) * a.o_tok + (int64_t)hq * a.o_head;
 #pragma unroll
         for (int t = 0; t < C::NT; ++t)
@@ -346,23 +367,36 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
             for (int g = 0; g < 4; ++g) {
                 u16x4 w;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = f2bf(o[t][4 * g + j] * inv);
+                for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(o[t][4 * g + j] * inv);
                 *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * h) = w;
             }
         if (h == 0)
             a.lse[(int64_t)hq * a.lse_stride + q0s + myq] = l > 0.f ? (m + __log2f(l)) * 0.69314718055994530942f : INFINITY;
     }
+#endif
 }
 
-namespace sa_launch {
-void fa_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
+template <bool F16, bool DROP>
+static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
         dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(64 * FwdV2<128>::NW);
-        if (D == 128) hipLaunchKernelGGL(fa_fwd_v2_kernel<128>, grid, block, 4 * FwdV2<128>::TILE, st, a);
-        else hipLaunchKernelGGL(fa_fwd_v2_kernel<64>, grid, block, 4 * FwdV2<64>::TILE, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+        else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
         return;
     }
     dim3 grid((max_q + 127) / 128, a.Hq, a.nseg), block(256);
-    hipLaunchKernelGGL(fa_fwd_kernel<32>, grid, block, 4 * 64 * 32 * 2, st, a);
+    hipLaunchKernelGGL((fa_fwd_kernel<32, F16, DROP>), grid, block, 4 * 64 * 32 * 2, st, a);
+}
+
+namespace sa_launch {
+void fa_fwd(const FwdArgs& a, int D, int max_q, bool f16, hipStream_t st) {
+    const bool drop = a.p_drop > 0.f;
+    if (f16) {
+        if (drop) launch_fwd<true, true>(a, D, max_q, st);
+        else launch_fwd<true, false>(a, D, max_q, st);
+    } else {
+        if (drop) launch_fwd<false, true>(a, D, max_q, st);
+        else launch_fwd<false, false>(a, D, max_q, st);
+    }
 }
 }  // namespace sa_launch

@@ -62,9 +62,12 @@ struct FwdArgs {
     const int* cu_q; const int* cu_k;
     int nseg, Hq, Hkv, causal, window;
     float scale_log2;
+    // attention-probability dropout (p_drop > 0): keep iff mix(seed, q head, q token, k token) >= drop_thr
+    float p_drop, rp_drop;  // rp_drop = 1 / (1 - p_drop)
+    uint32_t seed, drop_thr;
 };
 namespace sa_launch {
-void fa_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st);
+void fa_fwd(const FwdArgs& a, int D, int max_q, bool f16, hipStream_t st);
 }
 
 struct BwdArgs {
@@ -76,8 +79,22 @@ struct BwdArgs {
     const int* cu_q; const int* cu_k;
     int nseg, Hq, Hkv, causal, window;
     float scale, scale_log2;
+    float p_drop, rp_drop;
+    uint32_t seed, drop_thr;
 };
 namespace sa_launch {
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
-            hipStream_t st);
+            bool f16, hipStream_t st);
 }
+
+namespace sa_launch {
+// elementwise.hip: masked softmax, activations, dropout(+residual)
+void masked_softmax_fwd(int dtype, const void* x, const void* mask, void* y, int64_t rows, int N, int H, int Sq, int64_t mb,
+                        int64_t mh, int64_t mq, float scale, float fill, bool round, hipStream_t st);
+void masked_softmax_bwd(int dtype, const void* dy, const void* y, const void* mask, void* dx, int64_t rows, int N, int H,
+                        int Sq, int64_t mb, int64_t mh, int64_t mq, float scale, hipStream_t st);
+void act_fwd(int dtype, const void* x, void* y, int64_t n, int kind, hipStream_t st);
+void act_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t n, int kind, hipStream_t st);
+void dropout(int dtype, const void* x, const void* res, void* out, int64_t n, uint32_t seed, uint32_t thr, float rp,
+             hipStream_t st);
+}  // namespace sa_launch

@@ -1,7 +1,14 @@
+"""Activation functions of the MLP blocks (reference ``nn/activation_function.py``): the config enum is
+kept, the callables run the HIP elementwise kernels on GPU tensors (``scaling_amd.ops.elementwise``)."""
+from __future__ import annotations
+
 from enum import Enum
+from functools import partial
 from typing import Callable
 
 import torch
+
+from ...ops.elementwise import activation
 
 
 class ActivationFunction(Enum):
@@ -9,9 +16,11 @@ class ActivationFunction(Enum):
     SILU = "silu"
 
 
-def get_activation_function(activation_function: ActivationFunction) -> Callable[..., torch.Tensor]:
-    if activation_function == ActivationFunction.GELU:
-        return torch.nn.functional.gelu
-    if activation_function == ActivationFunction.SILU:
-        return torch.nn.functional.silu
-    raise NotImplementedError(str(activation_function))
+_KIND = {ActivationFunction.GELU: "gelu", ActivationFunction.SILU: "silu"}
+
+
+def get_activation_function(activation_function: ActivationFunction) -> Callable[[torch.Tensor], torch.Tensor]:
+    try:
+        return partial(activation, kind=_KIND[ActivationFunction(activation_function)])
+    except KeyError:
+        raise NotImplementedError(str(activation_function)) from None

@@ -274,13 +274,12 @@ class ParallelSelfAttention(torch.nn.Module):
             return None
         if self.lora_config is not None and not self.lora_merged_state:
             return None
-        if self.dropout_attention_probs > 0.0 and self.training:
-            return None
         pos = position_ids.reshape(-1) if position_ids is not None else None
         return attn_ops.rope_flash_attention(
             base, q, k, v, re.cos_table, re.sin_table, pos, re.dimensions, s, re.interleaved, cumulative_seq_lengths,
             max_seq_length if max_seq_length is not None else s, self.scaling_factor, self.causal,
-            self.local_attention_window_size if nl > 0 else None)
+            self.local_attention_window_size if nl > 0 else None,
+            dropout_p=self.dropout_attention_probs if self.training else 0.0)
 
     def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
         assert self.lora_config is not None

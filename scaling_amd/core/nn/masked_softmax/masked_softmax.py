@@ -1,11 +1,13 @@
 """Unfused masked softmax (reference ``masked_softmax.py:8-50``): optional fp32 upcast, multiply by
-``scale``, fill masked positions with -10000, softmax over the last dim."""
+``scale``, fill masked positions with -10000, softmax over the last dim.  On the GPU this is one HIP
+kernel per direction (``csrc/kernels/elementwise.hip``, fp32 math, rounding emulated for half inputs)."""
 from __future__ import annotations
 
 from typing import Optional
 
 import torch
 
+from ....ops.elementwise import masked_softmax
 from .masked_softmax_config import MaskedSoftmaxConfig, MaskedSoftmaxKernel
 
 
@@ -15,14 +17,7 @@ class MaskedSoftmaxTorch(torch.nn.Module):
         self.config = config
 
     def forward(self, x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
-        in_dtype = x.dtype
-        if self.config.softmax_in_fp32 and x.dtype != torch.float32:
-            x = x.float()
-        if self.config.scale != 1.0:
-            x = x * self.config.scale
-        x = x.masked_fill(mask.to(x.device), -10000.0)
-        probs = torch.softmax(x, dim=-1)
-        return probs.to(in_dtype) if self.config.softmax_in_fp32 else probs
+        return masked_softmax(x, mask, self.config.scale, self.config.softmax_in_fp32)
 
 
 class MaskedSoftmax(torch.nn.Module):

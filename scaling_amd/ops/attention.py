@@ -4,6 +4,10 @@ Replaces the reference's CUDA ``flash_attn_varlen_func`` dependency (``attention
 Layout is token-major ``[T, heads, head_dim]`` with arbitrary token/head strides, so q/k/v can be
 strided views of the fused QKV projection (no ``rearrange`` copies, no ``repeat_kv``).
 Backward is deterministic (dK/dV and dQ each owned by one workgroup, no float atomics).
+bf16 and fp16 operands run natively (fp32 inputs are computed in bf16).  Attention-probability dropout
+(reference ``flash_attn_varlen_func(dropout_p=...)``, ``attention.py:245-258``) is fused: the keep mask
+is a counter-based hash of (seed, q head, query token, key token) regenerated in the backward kernels,
+so no mask is stored; :func:`dropout_keep_mask` is its exact PyTorch twin.
 """
 from __future__ import annotations
 
@@ -15,8 +19,57 @@ import torch
 from ._ext import ext, use_native
 
 
-def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p: float = 0.0, training=False):
-    """Dense per-segment fp32 attention (numerical oracle and CPU path). q:[T,Hq,D], k/v:[Tk,Hk,D]."""
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(x: torch.Tensor, c: int) -> torch.Tensor:
+    """(x * c) mod 2^32 for int64 tensors holding uint32 values, without int64 overflow."""
+    lo, hi = c & 0xFFFF, c >> 16
+    return (x * lo + (((x * hi) & 0xFFFF) << 16)) & _M32
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = _mul32(x, 0x7FEB352D)
+    x = x ^ (x >> 15)
+    x = _mul32(x, 0x846CA68B)
+    return x ^ (x >> 16)
+
+
+def dropout_threshold(p: float) -> int:
+    return min(int(p * 4294967296.0), 0xFFFFFFFF)
+
+
+def dropout_keep_mask(seed: int, heads: torch.Tensor, q_tokens: torch.Tensor, k_tokens: torch.Tensor,
+                      p: float) -> torch.Tensor:
+    """Bool keep mask [H, Lq, Lk] of the fused flash-attention dropout (same hash as ``flash_attn.h``):
+    keep(h, q, k) = mix(mix(mix(seed ^ h*0x9e3779b9) + q) ^ k*0x85ebca6b) >= p * 2^32 (token indices are
+    positions in the packed [T] token dimension)."""
+    h = heads.long()
+    hs = _mix32((seed & _M32) ^ _mul32(h, 0x9E3779B9))  # [H]
+    row = _mix32((hs[:, None] + q_tokens.long()[None, :]) & _M32)  # [H, Lq]
+    kk = _mul32(k_tokens.long(), 0x85EBCA6B)  # [Lk]
+    return _mix32(row[:, :, None] ^ kk[None, None, :]) >= dropout_threshold(p)
+
+
+def dropout_seed(device: torch.device) -> int:
+    """Draws a 32-bit dropout seed from the device generator without a host<->device sync: the seed is a
+    function of the generator's (seed, offset), and the offset is advanced, so activation checkpointing
+    (which restores the RNG state before recomputing) and the TP-constant RNG tracker reproduce it."""
+    if device.type == "cuda":
+        gen = torch.cuda.default_generators[device.index if device.index is not None else torch.cuda.current_device()]
+        off = gen.get_offset()
+        gen.set_offset(off + 4)
+        base = gen.initial_seed()
+    else:
+        return int(torch.randint(0, 2**31 - 1, (1,)).item())
+    return int((base * 0x9E3779B97F4A7C15 + off * 0xBF58476D1CE4E5B9) >> 32) & _M32
+
+
+def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p: float = 0.0, training=False,
+                        dropout_seed_value: Optional[int] = None):
+    """Dense per-segment fp32 attention (numerical oracle and CPU path). q:[T,Hq,D], k/v:[Tk,Hk,D].
+    With ``dropout_seed_value`` the dropout mask is the fused kernel's (:func:`dropout_keep_mask`)."""
     Hq, Hk = q.shape[1], k.shape[1]
     rep = Hq // Hk
     out = torch.empty(q.shape[0], Hq, v.shape[2], dtype=q.dtype, device=q.device)
@@ -43,25 +96,32 @@ def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p
         p = torch.softmax(s, dim=-1)
         p = torch.nan_to_num(p, nan=0.0)
         if dropout_p > 0 and training:
-            p = torch.nn.functional.dropout(p, dropout_p)
+            if dropout_seed_value is not None:
+                keep = dropout_keep_mask(dropout_seed_value, torch.arange(Hq, device=q.device),
+                                         torch.arange(qs, qe, device=q.device), torch.arange(ks, ke, device=q.device),
+                                         dropout_p)
+                p = p * keep / (1.0 - dropout_p)
+            else:
+                p = torch.nn.functional.dropout(p, dropout_p)
         out[qs:qe] = torch.matmul(p, vi).transpose(0, 1).to(q.dtype)
     return out
 
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window):  # type: ignore[override]
-        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window)
+    def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window, p_drop=0.0, seed=0):  # type: ignore[override]
+        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed)
         ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
-        ctx.cfg = (max_q, max_k, scale, causal, window)
+        ctx.cfg = (max_q, max_k, scale, causal, window, p_drop, seed)
         return o
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         q, k, v, o, lse, cu_q, cu_k = ctx.saved_tensors
-        max_q, max_k, scale, causal, window = ctx.cfg
-        dq, dk, dv = ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window)
-        return dq, dk, dv, None, None, None, None, None, None, None
+        max_q, max_k, scale, causal, window, p_drop, seed = ctx.cfg
+        dq, dk, dv = ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, None, None, None,
+                                  p_drop, seed)
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None
 
 
 def _spec(t: torch.Tensor, base: torch.Tensor) -> tuple:
@@ -82,37 +142,37 @@ class _RopeFlashAttn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx: Any, base, specs, cos, sin, pos, rot_dim, seq_len, interleaved, cu_q, cu_k, max_q, max_k, scale,
-                causal, window):  # type: ignore[override]
+                causal, window, p_drop=0.0, seed=0):  # type: ignore[override]
         qi, ki, vi = (_view(base, sp) for sp in specs)
         q = ext().rope(qi, cos, sin, pos, rot_dim, seq_len, interleaved, False)
         k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
-        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window)
+        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed)
         ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
-        ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window)
+        ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed)
         return o
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
-        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window = ctx.cfg
+        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed = ctx.cfg
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
         v = _view(base, specs[2])
-        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv)
+        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed)
         ext().rope(dq, cos, sin, pos, rot_dim, seq_len, interleaved, True, dq)
         ext().rope(dk, cos, sin, pos, rot_dim, seq_len, interleaved, True, dk)
-        return (dbase,) + (None,) * 14
+        return (dbase,) + (None,) * 16
 
 
 def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor,
                          sin: torch.Tensor, pos: Optional[torch.Tensor], rot_dim: int, seq_len: int, interleaved: bool,
                          cu_seqlens: torch.Tensor, max_seqlen: int, softmax_scale: float, causal: bool = True,
-                         window: Optional[int] = None) -> Optional[torch.Tensor]:
+                         window: Optional[int] = None, dropout_p: float = 0.0) -> Optional[torch.Tensor]:
     """Fused RoPE + flash attention for q/k/v that are views tiling ``base`` exactly (the QKV GEMM output).
 
     Returns None when the fused path does not apply (CPU tensors, layouts that do not tile ``base``); the
     caller then runs rope and :func:`flash_attention` separately."""
-    if not (use_native(base) and base.is_contiguous() and base.dtype == torch.bfloat16):
+    if not (use_native(base) and base.is_contiguous() and base.dtype in (torch.bfloat16, torch.float16)):
         return None
     if q.numel() + k.numel() + v.numel() != base.numel():
         return None
@@ -123,8 +183,10 @@ def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v
     cq = cu_seqlens.to(torch.int32)
     p = None if pos is None else pos.reshape(-1).long()
     win = -1 if window is None else int(window)
+    seed = dropout_seed(base.device) if dropout_p > 0.0 else 0
     return _RopeFlashAttn.apply(base, specs, cos, sin, p, int(rot_dim), int(seq_len), bool(interleaved), cq, cq,
-                                int(max_seqlen), int(max_seqlen), float(softmax_scale), bool(causal), win)
+                                int(max_seqlen), int(max_seqlen), float(softmax_scale), bool(causal), win,
+                                float(dropout_p), seed)
 
 
 def flash_attention(
@@ -147,12 +209,19 @@ def flash_attention(
         max_seqlen_k = max_seqlen_q
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     win = -1 if window is None else int(window)
-    if use_native(q) and dropout_p == 0.0 or (use_native(q) and not training):
+    if use_native(q):
+        p_drop = float(dropout_p) if training else 0.0
+        in_dtype = q.dtype
+        if in_dtype not in (torch.bfloat16, torch.float16):  # fp32 runs through the bf16 kernel
+            q, k, v = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
         cq = cu_seqlens_q.to(torch.int32)
         ck = cu_seqlens_k.to(torch.int32)
         if max_seqlen_q is None:
             max_seqlen_q = int((cq[1:] - cq[:-1]).max().item())
         if max_seqlen_k is None:
             max_seqlen_k = int((ck[1:] - ck[:-1]).max().item())
-        return _FlashAttn.apply(q, k, v, cq, ck, int(max_seqlen_q), int(max_seqlen_k), float(scale), bool(causal), win)
+        seed = dropout_seed(q.device) if p_drop > 0.0 else 0
+        out = _FlashAttn.apply(q, k, v, cq, ck, int(max_seqlen_q), int(max_seqlen_k), float(scale), bool(causal), win,
+                               p_drop, seed)
+        return out if out.dtype == in_dtype else out.to(in_dtype)
     return attention_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, scale, causal, win, dropout_p, training)

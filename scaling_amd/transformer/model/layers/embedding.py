@@ -9,6 +9,7 @@ from typing import Any, Callable, Optional, TypeVar
 import torch
 
 from ....core import BaseLayer, Topology, VocabParallelEmbedding
+from ....ops.elementwise import dropout_add
 from ...context.config import TransformerArchitectureConfig
 from ...data.text_dataset_batch import TextDatasetBatch
 from .base import TransformerLayerIO
@@ -51,10 +52,12 @@ class BaseEmbeddingInput(BaseLayer[TextDatasetBatchGeneric, TransformerLayerIO, 
         self.cache: dict[int, Optional[torch.Tensor]] = {}
 
     def _tp_dropout(self, x: torch.Tensor) -> torch.Tensor:
+        if self.dropout.p == 0.0 or not self.training:
+            return x
         if self.topology is not None:
             with self.topology.model_parallel_constant_rng():
-                return self.dropout(x)
-        return self.dropout(x)
+                return dropout_add(x, None, self.dropout.p, True)
+        return dropout_add(x, None, self.dropout.p, True)
 
     def forward(self, x: TextDatasetBatchGeneric) -> TransformerLayerIO:
         st = x.inference_settings

@@ -8,6 +8,7 @@ from typing import Callable, Optional, Union
 import torch
 
 from ....core import ParallelMLP, ParallelSelfAttention, ParallelSwiGLUMLP, RotaryConfig, Topology, get_norm
+from ....ops.elementwise import dropout_add
 from ...context.config import MLPType, TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
 from .embedding import _device
@@ -89,13 +90,14 @@ class TransformerLayer(TransformerLayerBaseIO):
         assert hasattr(self, adapter_name), f"cannot use adapter '{adapter_name}' as it is not initialized"
         return getattr(self, adapter_name)(x)
 
-    def _dropout(self, drop: torch.nn.Dropout, x: torch.Tensor) -> torch.Tensor:
+    def _dropout_add(self, drop: torch.nn.Dropout, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+        """residual + dropout(x): one fused HIP pass on GPU, under the TP-constant RNG stream."""
         if drop.p == 0.0 or not self.training:
-            return x
+            return residual + x
         if self.topology is not None:
             with self.topology.model_parallel_constant_rng():
-                return drop(x)
-        return drop(x)
+                return dropout_add(x, residual, drop.p, True)
+        return dropout_add(x, residual, drop.p, True)
 
     def _attention_delta(self, hidden_state: torch.Tensor, cumulative_seq_lengths: torch.Tensor,
                          position_ids: torch.Tensor, use_cache: bool, reset_cache: bool, cache_index: int,
@@ -109,7 +111,7 @@ class TransformerLayer(TransformerLayerBaseIO):
         )
 
     def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor) -> torch.Tensor:
-        out = residual + self._dropout(self.dropout_mlp, self.mlp(normed))
+        out = self._dropout_add(self.dropout_mlp, self.mlp(normed), residual)
         if hasattr(self, "mlp_adapter_name"):
             out = out + self.apply_adapter(out, self.mlp_adapter_name)
         return out
@@ -120,7 +122,7 @@ class TransformerLayer(TransformerLayerBaseIO):
                         attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True) -> torch.Tensor:
         h = self._attention_delta(hidden_state, cumulative_seq_lengths, position_ids, use_cache, reset_cache, cache_index,
                                   attention_scores_manipulation, attentions_score_manipulation_log_additive)
-        out = hidden_state + self._dropout(self.dropout_attention, h)
+        out = self._dropout_add(self.dropout_attention, h, hidden_state)
         if hasattr(self, "attn_adapter_name"):
             out = out + self.apply_adapter(out, self.attn_adapter_name)
         return out

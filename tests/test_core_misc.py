@@ -222,3 +222,42 @@ def test_lora_merge_equivalence():
         attn.merge_lora_weights()
         y2 = attn(x, cumulative_seq_lengths=cu, position_ids=pos)
     torch.testing.assert_close(y1, y2, rtol=1e-4, atol=1e-5)
+
+
+def test_flash_dropout_mask_twin_matches_integer_reference():
+    """ops.attention.dropout_keep_mask (the PyTorch twin of the fused kernel mask) against plain Python
+    uint32 arithmetic of the same hash; keep rate = 1 - p."""
+    from scaling_amd.ops import attention as A
+
+    M = 0xFFFFFFFF
+
+    def mix(x):
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & M
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & M
+        return x ^ (x >> 16)
+
+    def keep(seed, h, q, k, p):
+        row = mix((mix(seed ^ ((h * 0x9E3779B9) & M)) + q) & M)
+        return mix(row ^ ((k * 0x85EBCA6B) & M)) >= A.dropout_threshold(p)
+
+    m = A.dropout_keep_mask(123456789, torch.arange(3), torch.arange(50, 66), torch.arange(100, 132), 0.3)
+    assert all(bool(m[h, i, j]) == keep(123456789, h, 50 + i, 100 + j, 0.3)
+               for h in range(3) for i in range(16) for j in range(32))
+    big = A.dropout_keep_mask(7, torch.arange(2), torch.arange(512), torch.arange(512), 0.1)
+    assert abs(big.float().mean().item() - 0.9) < 0.01
+
+
+def test_elementwise_cpu_paths_match_torch():
+    from scaling_amd.core.nn.activation_function import ActivationFunction, get_activation_function
+    from scaling_amd.ops import elementwise
+
+    x = torch.randn(100)
+    torch.testing.assert_close(get_activation_function(ActivationFunction.GELU)(x), torch.nn.functional.gelu(x))
+    torch.testing.assert_close(get_activation_function(ActivationFunction.SILU)(x), torch.nn.functional.silu(x))
+    assert torch.equal(elementwise.dropout_add(x, x, 0.5, training=False), x + x)
+    torch.manual_seed(0)
+    a = elementwise.dropout_add(x, None, 0.5, training=True)
+    torch.manual_seed(0)
+    assert torch.equal(a, torch.nn.functional.dropout(x, 0.5, training=True))

@@ -320,7 +320,7 @@ def test_sumsq_cast_unaligned(dtype, offset):
     torch.testing.assert_close(y, x.float() * 0.5, equal_nan=True)
 
 
-def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0):
+def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0, p_drop=0.0):
     torch.manual_seed(seed)
     T = sum(lens)
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device=DEV, dtype=torch.int32)
@@ -329,9 +329,16 @@ def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0)
     k = qkv[:, Hq : Hq + Hk].detach().requires_grad_(True)
     v = qkv[:, Hq + Hk :].detach().requires_grad_(True)
     scale = 1 / math.sqrt(D)
-    o = attention.flash_attention(q, k, v, cu, cu, max(lens), max(lens), scale, causal, None if window < 0 else window)
+    if p_drop > 0:
+        dseed = 12345 + seed
+        o = attention._FlashAttn.apply(q, k, v, cu, cu, max(lens), max(lens), scale, causal, window, p_drop, dseed)
+    else:
+        dseed = None
+        o = attention.flash_attention(q, k, v, cu, cu, max(lens), max(lens), scale, causal, None if window < 0 else window)
+    assert o.dtype == dtype
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
-    orf = attention.attention_reference(qr, kr, vr, cu, cu, scale, causal, window)
+    orf = attention.attention_reference(qr, kr, vr, cu, cu, scale, causal, window, dropout_p=p_drop, training=p_drop > 0,
+                                        dropout_seed_value=dseed)
     torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
     g = torch.randn_like(o)
     o.backward(g)
@@ -358,6 +365,64 @@ def test_flash_attention_window():
 
 def test_flash_attention_d32_noncausal_odd():
     _attn_case([65, 7], 2, 1, 32, False)
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_flash_attention_fp16(D):
+    _attn_case([200, 56], 4, 2, D, True, dtype=torch.float16)
+
+
+@pytest.mark.parametrize("D,dtype", [(128, torch.bfloat16), (64, torch.float16), (32, torch.bfloat16)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_dropout_matches_masked_reference(D, dtype, causal):
+    """Fused dropout: fwd + bwd equal the dense reference under the identical (hash) keep mask."""
+    _attn_case([190, 66], 4, 2, D, causal, dtype=dtype, p_drop=0.25)
+
+
+def test_flash_attention_dropout_rate_and_seed():
+    T, H, D = 1024, 4, 64
+    cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
+    keep = attention.dropout_keep_mask(7, torch.arange(H), torch.arange(T), torch.arange(T), 0.1)
+    assert abs(keep.float().mean().item() - 0.9) < 0.005
+    q, k = (torch.randn(T, H, D, device=DEV, dtype=torch.bfloat16) for _ in range(2))
+    v = torch.ones(T, H, D, device=DEV, dtype=torch.bfloat16)
+    # with V = 1 the output row sum of the (rescaled) dropped probabilities has mean ~1
+    o1 = attention._FlashAttn.apply(q, k, v, cu, cu, T, T, 0.125, False, -1, 0.1, 1)
+    o2 = attention._FlashAttn.apply(q, k, v, cu, cu, T, T, 0.125, False, -1, 0.1, 1)
+    o3 = attention._FlashAttn.apply(q, k, v, cu, cu, T, T, 0.125, False, -1, 0.1, 2)
+    assert torch.equal(o1, o2) and not torch.equal(o1, o3)
+    assert abs(o1.float().mean().item() - 1.0) < 0.02
+
+
+def test_rope_flash_attention_dropout_consistent():
+    """The fused RoPE+attention node with dropout equals rope -> flash attention with the same seed."""
+    from scaling_amd.core.nn.rotary import RotaryEmbedding
+    from scaling_amd.core.nn.rotary_config import RotaryConfig
+
+    torch.manual_seed(3)
+    T, Hq, Hk, D = 256, 4, 2, 64
+    re = RotaryEmbedding(RotaryConfig(dimensions=D, max_seq_length=T), device=torch.device(DEV))
+    base = torch.randn(T, (Hq + 2 * Hk) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
+
+    def split(b):
+        return (b[:, : Hq * D].view(T, Hq, D), b[:, Hq * D : (Hq + Hk) * D].view(T, Hk, D), b[:, (Hq + Hk) * D :].view(T, Hk, D))
+
+    gen = torch.cuda.default_generators[torch.cuda.current_device()]
+    st = gen.get_state()
+    o1 = attention.rope_flash_attention(base, *split(base), re.cos_table, re.sin_table, None, D, T, False, cu, T, 0.125,
+                                        True, None, dropout_p=0.2)
+    gen.set_state(st)
+    b2 = base.detach().clone().requires_grad_(True)
+    q2, k2, v2 = split(b2)
+    q2 = re.apply_tokens(q2, None, T)
+    k2 = re.apply_tokens(k2, None, T)
+    o2 = attention.flash_attention(q2, k2, v2, cu, cu, T, T, 0.125, True, None, dropout_p=0.2, training=True)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(o1)
+    o1.backward(g)
+    o2.backward(g)
+    torch.testing.assert_close(base.grad.float(), b2.grad.float(), atol=5e-2, rtol=5e-2)
 
 
 def test_flash_attention_deterministic():
@@ -391,3 +456,79 @@ def test_gemm_tn(M, N, K, accumulate):
     ref = A.float().t() @ B.float() + (C0.float() if accumulate else 0)
     torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
     assert not ext().gemm_tn_ok(A[:, :200], B, C[:200])
+
+
+# ---------------------------------------------------------------- masked softmax / activations / dropout
+from scaling_amd.ops import elementwise  # noqa: E402
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("seq_len", [128, 200, 1024])
+@pytest.mark.parametrize("scale", [1.0, 0.5])
+@pytest.mark.parametrize("fp32", [False, True])
+def test_masked_softmax_matches_torch(dtype, seq_len, scale, fp32):
+    """Reference tolerance (tests/core/test_nn/test_masked_softmax.py:53): mean |delta| < 4e-6."""
+    from scaling_amd.core.nn.attention import cumulative_seq_lengths_to_dense_attention_mask
+
+    torch.manual_seed(42)
+    x = torch.randn(2, 4, seq_len, seq_len, device=DEV, dtype=dtype)
+    cu = torch.tensor([0, seq_len // 3, seq_len, 2 * seq_len], device=DEV)
+    mask = cumulative_seq_lengths_to_dense_attention_mask(cu, seq_len, causal=True)
+    y = elementwise.masked_softmax(x, mask, scale, fp32)
+    ref = elementwise.masked_softmax_reference(x, mask, scale, fp32)
+    assert y.dtype == ref.dtype == dtype
+    assert (y.float() - ref.float()).abs().mean().item() < 4e-6
+    xg = x.detach().float().requires_grad_(True)
+    xh = x.detach().clone().requires_grad_(True)
+    g = torch.randn_like(x)
+    elementwise.masked_softmax(xh, mask, scale, fp32).backward(g)
+    elementwise.masked_softmax_reference(xg, mask, scale, True).backward(g.float())
+    torch.testing.assert_close(xh.grad.float(), xg.grad, atol=2e-2 if dtype != torch.float32 else 1e-5, rtol=2e-2)
+
+
+def test_masked_softmax_fully_masked_rows_uniform():
+    x = torch.randn(1, 2, 8, 24, device=DEV, dtype=torch.bfloat16)
+    mask = torch.ones(1, 1, 8, 24, dtype=torch.bool, device=DEV)
+    y = elementwise.masked_softmax(x, mask, 1.0, False)
+    torch.testing.assert_close(y.float(), torch.full_like(y.float(), 1 / 24), atol=1e-3, rtol=0)
+
+
+@pytest.mark.parametrize("kind", ["gelu", "silu", "gelu_tanh"])
+@pytest.mark.parametrize("dtype,n", [(torch.bfloat16, 4096 * 3 + 5), (torch.float32, 1000), (torch.float16, 64)])
+def test_activation(kind, dtype, n):
+    torch.manual_seed(0)
+    x = (torch.randn(n, device=DEV, dtype=dtype) * 3).requires_grad_(True)
+    xr = x.detach().double().requires_grad_(True)
+    y = elementwise.activation(x, kind)
+    f = {"gelu": lambda t: torch.nn.functional.gelu(t), "silu": torch.nn.functional.silu,
+         "gelu_tanh": lambda t: torch.nn.functional.gelu(t, approximate="tanh")}[kind]
+    yr = f(xr)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    torch.testing.assert_close(y.double(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.double())
+    torch.testing.assert_close(x.grad.double(), xr.grad, atol=tol * 3, rtol=tol * 3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_dropout_add(dtype, with_res):
+    torch.manual_seed(0)
+    n = 1 << 20
+    x = torch.randn(n + 3, device=DEV, dtype=dtype)[3:].requires_grad_(True)  # unaligned view
+    res = torch.randn(n, device=DEV, dtype=dtype).requires_grad_(True) if with_res else None
+    out = elementwise._DropoutAdd.apply(x, res, 0.3, 99)
+    plain = elementwise._DropoutAdd.apply(x.detach(), None, 0.3, 99)  # same seed -> same mask
+    kept = plain != 0
+    assert abs(kept.float().mean().item() - 0.7) < 0.005
+    torch.testing.assert_close(plain.float(), torch.where(kept, x.detach().float() / 0.7, 0.0), atol=1e-2, rtol=1e-2)
+    if with_res:
+        torch.testing.assert_close(out.float(), res.detach().float() + plain.float(), atol=3e-2, rtol=1e-2)
+    out2 = elementwise._DropoutAdd.apply(x, res, 0.3, 99)
+    assert torch.equal(out, out2)
+    g = torch.randn_like(out)
+    out.backward(g)
+    torch.testing.assert_close(x.grad.float(), torch.where(kept, g / 0.7, 0.0).float(), atol=1e-2, rtol=1e-2)
+    if with_res:
+        assert torch.equal(res.grad, g)
