@@ -352,6 +352,19 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
     a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)Hk; a.causal = causal ? 1 : 0; a.window = (int)window;
     a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
     a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
+    // GQA head split of the dK/dV sweep: causal/windowed work is triangular, and with few (kv head, key
+    // block) workgroups the heaviest one bounds the kernel; splitting the q-head group evens it out
+    a.hsplit = 1; a.Tk = (int)Tk;
+    const int grp = (int)(H / Hk);
+    const int64_t kblocks = (max_k + 127) / 128;
+    if (causal || window >= 0)
+        while (a.hsplit < grp && grp % (2 * a.hsplit) == 0 && Hk * a.hsplit * a.nseg * kblocks < 1024) a.hsplit *= 2;
+    at::Tensor part;
+    if (a.hsplit > 1) {
+        part = at::empty({2, a.hsplit, Tk, Hk, D}, q.options().dtype(at::kFloat));
+        a.dk_part = part[0].data_ptr<float>();
+        a.dv_part = part[1].data_ptr<float>();
+    }
     if (T > 0 && a.nseg > 0)
         sa_launch::fa_bwd(a, (const uint16_t*)o.data_ptr(), o.stride(0), o.stride(1), T, (int)D, (int)max_q, (int)max_k,
                           q.scalar_type() == at::kHalf, cur_stream());

@@ -110,11 +110,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
 // resource range land as zeros.  No staging registers, no ds_write; completion is the vmcnt(0)
 // the compiler places before the next __syncthreads().
 typedef __attribute__((address_space(3))) void lds_void;
-template <int D, int W>
+template <int D, int W, int ROWS = 64>
 struct DmaTile {
-    static constexpr int PIECES = 64 * D * 2 / 1024;
-    static constexpr int NPW = PIECES / W;
-    static_assert(NPW >= 1 && NPW * W == PIECES, "tile pieces must split evenly across waves");
+    static constexpr int PIECES = ROWS * D * 2 / 1024;
+    static constexpr int NPW = (PIECES + W - 1) / W;
+    static_assert(PIECES >= 1 && (PIECES % W == 0 || PIECES < W), "tile pieces must split evenly across waves");
     int voff[NPW];
     __device__ __forceinline__ void init(int wave, int lane, int64_t tok) {
 #pragma unroll
@@ -128,12 +128,13 @@ struct DmaTile {
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(base, (uint32_t)max(rows, 0) * (uint32_t)tok * 2u);
 #pragma unroll
         for (int i = 0; i < NPW; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(tile + (wave_u + W * i) * 1024), 16, voff[i], 0, 0, 0);
+            if (PIECES >= W || wave_u + W * i < PIECES)  // wave-uniform
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(tile + (wave_u + W * i) * 1024), 16, voff[i], 0, 0, 0);
     }
 };
 
-template <int D, int W>
-__device__ __forceinline__ void dma_load(const DmaTile<D, W>& t, const void* base, int64_t tok, int rows, char* tile,
+template <int D, int W, int R>
+__device__ __forceinline__ void dma_load(const DmaTile<D, W, R>& t, const void* base, int64_t tok, int rows, char* tile,
                                          int wave_u) {
     t.load(base, tok, rows, tile, wave_u);
 }

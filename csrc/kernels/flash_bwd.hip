@@ -49,35 +49,43 @@ __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const E* __restrict__ o
 // block offsets are compile-time immediates (loops unrolled per buffer).
 template <int D>
 struct LdsOffsets {
-    int row[D / 16];
-    int tr[D / 32][2];
+    // swz(r, c) = c ^ F(r): a chunk index 2ks + h (row reads) or 4t + low (transposed reads) XOR F(r)
+    // splits into a per-lane base plus (const ^ per-lane high bits), so 6 registers replace 16 offsets
+    int row_base, row_hi;
+    int tr_base[2], tr_hi[2];
     __device__ __forceinline__ void init(int lane) {
         const int h = lane >> 5, r = lane & 31, g = (lane >> 4) & 1, i = lane & 15;
+        const int fr = swz<D>(r, 0);
+        row_base = r * D * 2 + 16 * (h ^ (fr & 1));
+        row_hi = 16 * (fr & ~1);
+        const int low = 2 * g + ((i & 3) >> 1);
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) row[ks] = lds_off<D>(r, 16 * ks + 8 * h);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) {
-            tr[t][0] = lds_off<D>(4 * h + (i >> 2), 32 * t + 16 * g + 4 * (i & 3));
-            tr[t][1] = lds_off<D>(4 * h + (i >> 2) + 8, 32 * t + 16 * g + 4 * (i & 3));
+        for (int x = 0; x < 2; ++x) {
+            const int tr_row = 4 * h + (i >> 2) + 8 * x;
+            const int ft = swz<D>(tr_row, 0);
+            tr_base[x] = tr_row * D * 2 + 16 * (low ^ (ft & 3)) + (((4 * (i & 3)) & 7) << 1);
+            tr_hi[x] = 16 * (ft & ~3);
         }
     }
+    __device__ __forceinline__ int row(int ks) const { return row_base + ((32 * ks) ^ row_hi); }
+    __device__ __forceinline__ int tr(int t, int x) const { return tr_base[x] + ((64 * t) ^ tr_hi[x]); }
 };
 template <int D>
 __device__ __forceinline__ bf16x8 rd_row(const char* tile, int imm, int off) {
     return *reinterpret_cast<const bf16x8*>(tile + imm + off);
 }
 template <int D>
-__device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const int (&tr)[2]) {
-    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + tr[0]));
-    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + tr[1]));
+__device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffsets<D>& lo, int t) {
+    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + lo.tr(t, 0)));
+    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + lo.tr(t, 1)));
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// dK / dV: workgroup = 4 waves x 32 keys of one (segment, kv head); the key is on the MFMA lane: each
-// wave reads its K and V rows (B operands) from the workgroup's K/V image for the whole sweep over the
-// GQA group's q heads x 64-query tiles.  Q, dO, lse2 (= lse * log2 e) and delta arrive by LDS-DMA
-// into a double buffer (no staging registers), so the 256-register cap holds S / dP in arch VGPRs
-// and dK / dV never bounce through v_accvgpr moves.  Per 32-query block:
+// dK / dV: workgroup = 4 waves x 32 keys of one (segment, kv head); the key is on the MFMA lane.  Each
+// wave keeps its 32 K rows as register-resident B-operand fragments and reads its V rows from the
+// workgroup's V image (LDS, loaded once); it sweeps the GQA (sub)group's q heads x 32-query tiles.  Q, dO,
+// lse2 (= lse * log2 e) and delta arrive by LDS-DMA into a double buffer.  LDS = V image + 2 x 32-query
+// buffers (65 KiB at D = 128), so two workgroups (2 waves / SIMD) share a CU.  Per 32-query tile:
 //   S = Q K^T, dP = dO V^T (row reads), p = exp2(S c - lse2), dS = p (dP - delta),
 //   dV^T += dO^T P, dK^T += Q^T dS (transposed reads; P / dS accumulators are the B operands).
 // Query rows past the segment arrive as zeros (Q = dO = 0, lse2 = delta = 0) and contribute nothing.
@@ -85,14 +93,15 @@ template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int TILE = 64 * D * 2, BUF = 2 * TILE + 512, NKS = D / 16, NT = D / 32;
-    // grid (Hkv, nseg, key blocks): key block slowest so causal work is issued heaviest-first
-    const int seg = blockIdx.y, hk = blockIdx.x;
+    constexpr int QT = 32, TILE = QT * D * 2, BUF = 2 * TILE + 512, VIMG = 128 * D * 2, NKS = D / 16, NT = D / 32;
+    // grid (Hkv * hsplit, nseg, key blocks): key block slowest so causal work is issued heaviest-first
+    const int seg = blockIdx.y, hk = blockIdx.x / a.hsplit, sub = blockIdx.x % a.hsplit;
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int kwg0 = blockIdx.z * 128;
     if (kwg0 >= Lk) return;
-    const int grp = a.Hq / a.Hkv;
+    const int grp = a.Hq / a.Hkv / a.hsplit;  // q heads swept by this workgroup: hk * Hq/Hkv + sub * grp + [0, grp)
+    const int h0 = hk * (a.Hq / a.Hkv) + sub * grp;
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, lk = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int off = Lk - Lq;
@@ -104,36 +113,37 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         qhi = min(Lq, klast - off + a.window + 1);
         if (!a.causal) qlo = max(0, kwg0 - off - a.window);
     }
-    qlo = (qlo / 64) * 64;
-    const int ntq = qhi > qlo ? (qhi - qlo + 63) / 64 : 0;
+    qlo = (qlo / QT) * QT;
+    const int ntq = qhi > qlo ? (qhi - qlo + QT - 1) / QT : 0;
     const int nwork = ntq * grp;
 
-    char* kimg = smem + 2 * BUF;  // K rows [0, 128) then V rows [0, 128)
+    char* vimg = smem;  // V rows [kwg0, kwg0 + 128)
     {
-        DmaTile<D, 4> dk_, dv_;
-        dk_.init(wave, lane, a.k_tok);
+        DmaTile<D, 4> dv_;
         dv_.init(wave, lane, a.v_tok);
-        const u16* kb = a.k + (int64_t)(k0s + kwg0) * a.k_tok + (int64_t)hk * a.k_head;
         const u16* vb = a.v + (int64_t)(k0s + kwg0) * a.v_tok + (int64_t)hk * a.v_head;
-        dk_.load(kb, a.k_tok, Lk - kwg0, kimg, wave);
-        dk_.load(kb + 64 * a.k_tok, a.k_tok, Lk - kwg0 - 64, kimg + TILE, wave);
-        dv_.load(vb, a.v_tok, Lk - kwg0, kimg + 2 * TILE, wave);
-        dv_.load(vb + 64 * a.v_tok, a.v_tok, Lk - kwg0 - 64, kimg + 3 * TILE, wave);
+        dma_load(dv_, vb, a.v_tok, Lk - kwg0, vimg, wave);
+        dma_load(dv_, vb + 64 * a.v_tok, a.v_tok, Lk - kwg0 - 64, vimg + 64 * D * 2, wave);
     }
-    const char* kw_img = kimg + 32 * wave * D * 2;
-    const char* vw_img = kimg + 2 * TILE + 32 * wave * D * 2;
+    const char* vw_img = vimg + 32 * wave * D * 2;
+    bf16x8 kf[NKS];  // lane: key kw0 + (lane & 31), dims 16 ks + 8 h .. + 7
+    {
+        const u16* kp = a.k + (int64_t)(k0s + min(mykey, Lk - 1)) * a.k_tok + (int64_t)hk * a.k_head;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) kf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(kp + 16 * ks + 8 * h));
+    }
     LdsOffsets<D> lo;
     lo.init(lane);
-    DmaTile<D, 4> tq, td;
+    DmaTile<D, 4, QT> tq, td;
     tq.init(wave, lane, a.q_tok);
     td.init(wave, lane, a.do_tok);
     auto issue = [&](int w, char* buf) {
-        const int gi = w / ntq, qt = qlo + (w % ntq) * 64, hq = hk * grp + gi;
-        tq.load(a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
-        td.load(a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
-        if (wave == 0) {  // 64 lse2 then 64 delta: one dword per lane each
+        const int gi = w / ntq, qt = qlo + (w % ntq) * QT, hq = h0 + gi;
+        dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
+        dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
+        if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
             const int64_t ix = (int64_t)hq * a.lse_stride + q0s + qt;
-            const uint32_t nb = (uint32_t)max(min(64, Lq - qt), 0) * 4u;
+            const uint32_t nb = (uint32_t)max(min(QT, Lq - qt), 0) * 4u;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
         }
@@ -147,74 +157,70 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const char* DO = Q + TILE;
         const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
         const float* DL = LS + 64;
-        const int qt = qlo + (w % ntq) * 64;
+        const int qt = qlo + (w % ntq) * QT;
         uint32_t hs = 0;
-        if constexpr (DROP) hs = drop_head(a.seed, hk * grp + w / ntq);
+        if constexpr (DROP) hs = drop_head(a.seed, h0 + w / ntq);
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
-                               (a.window >= 0 && (kw0 < qt + 63 + off - a.window || (!a.causal && kw0 + 31 > qt + off + a.window)));
+                               (a.window >= 0 && (kw0 < qt + QT - 1 + off - a.window || (!a.causal && kw0 + 31 > qt + off + a.window)));
+        f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            f32x16 s = f32x16{}, dp = f32x16{};
+        for (int ks = 0; ks < NKS; ++ks) {
+            s = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], s);
+            dp = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dp);
+        }
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                s = mma<F16>(rd_row<D>(Q, 32 * b * D * 2, lo.row[ks]), rd_row<D>(kw_img, 0, lo.row[ks]), s);
-                dp = mma<F16>(rd_row<D>(DO, 32 * b * D * 2, lo.row[ks]), rd_row<D>(vw_img, 0, lo.row[ks]), dp);
+        for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        // query of register j: qt + 4h + crow(j)
+        int mlo = -1 << 30, mhi = 1 << 30;
+        if (need_mask) {
+            const int rel = mykey - off - qt - 4 * h;
+            if (a.causal) mlo = rel;                  // key <= q + off
+            if (a.window >= 0) {
+                mhi = rel + a.window;                 // key >= q + off - window
+                if (!a.causal) mlo = rel - a.window;  // key <= q + off + window
             }
+        }
 #pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            // query of register j: qt + 32b + 4h + crow(j)
-            int mlo = -1 << 30, mhi = 1 << 30;
-            if (need_mask) {
-                const int rel = mykey - off - qt - 32 * b - 4 * h;
-                if (a.causal) mlo = rel;                  // key <= q + off
-                if (a.window >= 0) {
-                    mhi = rel + a.window;                 // key >= q + off - window
-                    if (!a.causal) mlo = rel - a.window;  // key <= q + off + window
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 8 * g + 4 * h);
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = 4 * g + j;
+                float p = fast_exp2(__builtin_fmaf(s[r], c2, -l4[j]));
+                if (need_mask) p = (crow(r) >= mlo && crow(r) <= mhi) ? p : 0.f;
+                if constexpr (DROP) {  // dV sees the dropped P; dS = P (Z dP / (1-p) - delta)
+                    const bool keep = drop_keep(drop_row(hs, q0s + qt + 4 * h + crow(r)), k0s + mykey, a.drop_thr);
+                    s[r] = keep ? p * a.rp_drop : 0.f;
+                    dp[r] = p * ((keep ? dp[r] * a.rp_drop : 0.f) - d4[j]);
+                } else {
+                    s[r] = p;
+                    dp[r] = p * (dp[r] - d4[j]);
                 }
             }
+        }
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 32 * b + 8 * g + 4 * h);
-                const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + 32 * b + 8 * g + 4 * h);
+        for (int ss = 0; ss < 2; ++ss) {
+            const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
+            const int kb = 16 * ss * D * 2;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = 4 * g + j;
-                    float p = fast_exp2(__builtin_fmaf(s[r], c2, -l4[j]));
-                    if (need_mask) p = (crow(r) >= mlo && crow(r) <= mhi) ? p : 0.f;
-                    if constexpr (DROP) {  // dV sees the dropped P; dS = P (Z dP / (1-p) - delta)
-                        const int qtok = q0s + qt + 32 * b + 4 * h + crow(r);
-                        const bool keep = drop_keep(drop_row(hs, qtok), k0s + mykey, a.drop_thr);
-                        s[r] = keep ? p * a.rp_drop : 0.f;
-                        dp[r] = p * ((keep ? dp[r] * a.rp_drop : 0.f) - d4[j]);
-                    } else {
-                        s[r] = p;
-                        dp[r] = p * (dp[r] - d4[j]);
-                    }
-                }
+            for (int t = 0; t < NT; ++t) {
+                dv[t] = mma<F16>(rd_tr<D>(DO, kb, lo, t), pb, dv[t]);
+                dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo, t), db, dk[t]);
             }
+        }
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
-                const int kb = (32 * b + 16 * ss) * D * 2;
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    dv[t] = mma<F16>(rd_tr<D>(DO, kb, lo.tr[t]), pb, dv[t]);
-                    dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo.tr[t]), db, dk[t]);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4 * NT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            }
+        for (int i = 0; i < 4 * NT; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
         }
     };
 
-    char* buf0 = smem;
-    char* buf1 = smem + BUF;
+    char* buf0 = smem + VIMG;
+    char* buf1 = buf0 + BUF;
     if (nwork > 0) issue(0, buf0);
     __syncthreads();
     int w = 0;
@@ -229,21 +235,40 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     if (w < nwork) tile(buf0, w);
 
     if (mykey < Lk) {
-        u16* kp = a.dk + (int64_t)(k0s + mykey) * a.dk_tok + (int64_t)hk * a.dk_head;
-        u16* vp = a.dv + (int64_t)(k0s + mykey) * a.dv_tok + (int64_t)hk * a.dv_head;
+        if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel
+            const int64_t pix = (((int64_t)sub * a.Tk + k0s + mykey) * a.Hkv + hk) * D;
+            float* kp = a.dk_part + pix;
+            float* vp = a.dv_part + pix;
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+            for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                u16x4 wk, wv;
+                for (int g = 0; g < 4; ++g) {
+                    f32x4 wk, wv;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    wk[j] = f2t<F16>(dk[t][4 * g + j] * a.scale);
-                    wv[j] = f2t<F16>(dv[t][4 * g + j]);
+                    for (int j = 0; j < 4; ++j) {
+                        wk[j] = dk[t][4 * g + j] * a.scale;
+                        wv[j] = dv[t][4 * g + j];
+                    }
+                    *reinterpret_cast<f32x4*>(kp + 32 * t + 8 * g + 4 * h) = wk;
+                    *reinterpret_cast<f32x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
                 }
-                *reinterpret_cast<u16x4*>(kp + 32 * t + 8 * g + 4 * h) = wk;
-                *reinterpret_cast<u16x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
-            }
+        } else {
+            u16* kp = a.dk + (int64_t)(k0s + mykey) * a.dk_tok + (int64_t)hk * a.dk_head;
+            u16* vp = a.dv + (int64_t)(k0s + mykey) * a.dv_tok + (int64_t)hk * a.dv_head;
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    u16x4 wk, wv;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        wk[j] = f2t<F16>(dk[t][4 * g + j] * a.scale);
+                        wv[j] = f2t<F16>(dv[t][4 * g + j]);
+                    }
+                    *reinterpret_cast<u16x4*>(kp + 32 * t + 8 * g + 4 * h) = wk;
+                    *reinterpret_cast<u16x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
+                }
+        }
     }
 #endif
 }
@@ -318,8 +343,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
             f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row[ks]), qf[ks], s);
-                dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row[ks]), df[ks], dp);
+                s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row(ks)), qf[ks], s);
+                dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row(ks)), df[ks], dp);
             }
             // key of register j: kt + 32b + 4h + crow(j)
             int hi = 1 << 30, low = -1 << 30;
@@ -346,7 +371,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
                 const bf16x8 db = pack_acc_t<F16>(dp, ss);
                 const int kb = (32 * b + 16 * ss) * D * 2;
 #pragma unroll
-                for (int t = 0; t < NT; ++t) dq[t] = mma<F16>(rd_tr<D>(K, kb, lo.tr[t]), db, dq[t]);
+                for (int t = 0; t < NT; ++t) dq[t] = mma<F16>(rd_tr<D>(K, kb, lo, t), db, dq[t]);
             }
         }
     };
@@ -382,11 +407,39 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
 #endif
 }
 
+// dK/dV = sum of the hsplit fp32 partials (fixed order: deterministic), cast into the strided outputs.
+template <int D, bool F16>
+__global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = (int64_t)a.Tk * a.Hkv * (D / 8);
+    if (gid >= per) return;
+    const int c = (int)(gid % (D / 8));
+    const int64_t th = gid / (D / 8);
+    const int hk = (int)(th % a.Hkv);
+    const int64_t tok = th / a.Hkv;
+    const int64_t pstride = (int64_t)a.Tk * a.Hkv * D;
+    float sk[8] = {}, sv[8] = {};
+    for (int s = 0; s < a.hsplit; ++s) {
+        const float* kp = a.dk_part + s * pstride + th * D + 8 * c;
+        const float* vp = a.dv_part + s * pstride + th * D + 8 * c;
+        float x[8], y[8];
+        V8<float>::ld(kp, x);
+        V8<float>::ld(vp, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sk[j] += x[j]; sv[j] += y[j]; }
+    }
+    u16x8 wk, wv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { wk[j] = fa::f2t<F16>(sk[j]); wv[j] = fa::f2t<F16>(sv[j]); }
+    *reinterpret_cast<u16x8*>(a.dk + tok * a.dk_tok + (int64_t)hk * a.dk_head + 8 * c) = wk;
+    *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
+}
+
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
-        dim3 grid(a.Hkv, a.nseg, (max_k + 127) / 128);
-        const size_t lds = 2 * (2 * 64 * D * 2 + 512) + 4 * 64 * D * 2;
+        dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
+        const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
@@ -397,6 +450,13 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
+    }
+    if (a.hsplit > 1) {
+        const int64_t threads = (int64_t)a.Tk * a.Hkv * (D / 8);
+        const int grid = (int)((threads + 255) / 256);
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_reduce_kernel<128, F16>), grid, 256, 0, st, a);
+        else if (D == 64) hipLaunchKernelGGL((fa_bwd_reduce_kernel<64, F16>), grid, 256, 0, st, a);
+        else hipLaunchKernelGGL((fa_bwd_reduce_kernel<32, F16>), grid, 256, 0, st, a);
     }
 }
 

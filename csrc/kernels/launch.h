@@ -81,6 +81,11 @@ struct BwdArgs {
     float scale, scale_log2;
     float p_drop, rp_drop;
     uint32_t seed, drop_thr;
+    // dK/dV GQA head split: hsplit workgroups per (kv head, key block) each sweep grp/hsplit q heads and
+    // (hsplit > 1) write fp32 partials [hsplit][Tk][Hkv][D] that fa_bwd_reduce sums (causal load balance)
+    int hsplit, Tk;
+    float* dk_part;
+    float* dv_part;
 };
 namespace sa_launch {
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
