@@ -128,6 +128,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
             if topology.is_last_pipe_parallel_rank:
                 self.communicator_loss_out = PipeCommunicator(dev, recv_grads=False, recv_data=False)
         self.profiler = Profiler(config=profiler_config, topology=topology)
+        self._param_sync_optimizer: Optional[BaseOptimizer] = None
         self.step_timer = _StepTimer()
         self.broadcast_model()
 
@@ -175,9 +176,15 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         return int(t[0].item()), int(t[1].item())
 
     # ------------------------------------------------------------------ forward
+    def _param_sync(self, layer: Any) -> None:
+        """Waits for the ZeRO all-gather of this layer's parameters (issued asynchronously by the optimizer)."""
+        if self._param_sync_optimizer is not None:
+            self._param_sync_optimizer.wait_param_sync(layer)
+
     def _forward_tuple_input(self, *args: Any) -> Any:
         x = self._layers[0].tuple_to_input(tuple(args))
         for layer in self._layers:
+            self._param_sync(layer)
             x = layer(x)
         return x
 
@@ -187,9 +194,11 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
             return checkpoint_with_rng(self._forward_tuple_input, self.topology, True, *self._layers[0].input_to_tuple(x))
         if self.training and ac == ActivationCheckpointingType.EVERY_LAYER:
             for layer in self._layers:
+                self._param_sync(layer)
                 x = checkpoint_with_rng(layer._forward_tuple_input, self.topology, True, *layer.input_to_tuple(x))
             return x
         for layer in self._layers:
+            self._param_sync(layer)
             x = layer(x)
         return x
 
@@ -227,6 +236,9 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         self._layers.train()
         self.pipe_buffer.reset()
         self.profiler.step()
+        if self._param_sync_optimizer is not optimizer:
+            optimizer.attach_param_sync(self._layers)
+            self._param_sync_optimizer = optimizer
         last_mb = self.topology.config.gradient_accumulation_steps - 1
         opt_out = None
         for ins in self.train_instructions:
@@ -268,6 +280,8 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         self._layers.eval()
         self.pipe_buffer.reset()
         self.profiler.step()
+        if self._param_sync_optimizer is not None:
+            self._param_sync_optimizer.wait_param_sync()
         for ins in self.evaluation_instructions:
             name, mb, buf = get_timer_args(ins)
             with self.profiler.time(name, mb, buf):
@@ -293,6 +307,8 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
 
     def run_instructions(self, instructions: list[InstructionBase], sync_batch_to_model_parallel: Callable,
                          collect_outputs_from_model_parallel: Callable, batch: Any = None) -> Any:
+        if self._param_sync_optimizer is not None:
+            self._param_sync_optimizer.wait_param_sync()
         ins = None
         for ins in instructions:
             if isinstance(ins, InstructionStoreMicroBatch):

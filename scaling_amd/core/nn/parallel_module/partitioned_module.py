@@ -120,6 +120,9 @@ class PipePartitionedModule(torch.nn.Module):
 
     # ------------------------------------------------------------------ checkpoint
     def save_checkpoint(self, dir_: Union[Path, str], separate_file_for_parameters: Optional[list[str]] = None) -> None:
+        opt = getattr(self, "_param_sync_optimizer", None)
+        if opt is not None:  # parameters may still be in flight (async ZeRO all-gather)
+            opt.wait_param_sync()
         if self.topology is not None and self.topology.data_parallel_rank != 0:
             return
         dir_ = Path(dir_)

@@ -53,3 +53,10 @@ class BaseOptimizer(ABC):
 
     def finish_grad_sync(self) -> None:
         pass
+
+    # hooks used by the engine to overlap the ZeRO parameter all-gather with the next forward pass
+    def attach_param_sync(self, layers: Any) -> None:
+        pass
+
+    def wait_param_sync(self, layer: Optional[Any] = None) -> None:
+        pass

@@ -15,7 +15,11 @@ MI355X-first differences:
 * norm + overflow of all gradients come from one fused HIP reduction and ONE world all-reduce —
   a single host sync per step (the reference syncs once per parameter);
 * the update is one fused HIP AdamW launch per bucket (fp32 master + moments, writes the bf16
-  parameter copy in the same pass).
+  parameter copy in the same pass);
+* with ZeRO the parameter all-gather of bucket b is issued on the side stream right after bucket b's
+  AdamW and completes asynchronously: each pipeline layer's next forward waits only for the buckets
+  holding its parameters (``attach_param_sync``/``wait_param_sync``), so the gather of late layers
+  overlaps the forward of early ones.
 """
 from __future__ import annotations
 
@@ -62,6 +66,8 @@ class Optimizer(BaseOptimizer):
         self._pending: list[list[int]] = [list(g.bucket_param_count) for g in parameter_groups]
         self._armed = False
         self._deferred = self._deferred_buckets()
+        self._ag_events: dict[tuple[int, int], Any] = {}
+        self._layer_buckets: dict[int, list[tuple[int, int]]] = {}
         self._hooks = []
         if self.dp > 1 and config.overlap_grad_reduce and not topology.config.sequence_parallel:
             for gi, g in enumerate(parameter_groups):
@@ -197,7 +203,56 @@ class Optimizer(BaseOptimizer):
         v = vals.tolist()
         return float(v[0]), float(v[1])
 
+    # ------------------------------------------------------------------ parameter all-gather overlap
+    def _async_param_gather(self) -> bool:
+        return bool(self.config.zero and self.dp > 1 and self._comm_stream is not None and self.config.overlap_param_gather)
+
+    def attach_param_sync(self, layers: Any) -> None:
+        """Records, per pipeline layer, the (group, bucket) pairs holding its parameters."""
+        where: dict[int, list[tuple[int, int]]] = {}
+        for gi, g in enumerate(self.parameter_groups):
+            for pi, p in enumerate(g.parameters_original):
+                where.setdefault(id(p), []).extend((gi, b) for b in g.param_buckets[pi])
+        self._layer_buckets = {}
+        for layer in layers:
+            keys = sorted({k for p in layer.parameters() for k in where.get(id(p), [])})
+            self._layer_buckets[id(layer)] = keys
+
+    def wait_param_sync(self, layer: Optional[Any] = None) -> None:
+        """Makes the current stream wait for the pending all-gathers of `layer`'s buckets (all if None)."""
+        if not self._ag_events:
+            return
+        if layer is None:
+            keys = list(self._ag_events.keys())
+        else:
+            keys = self._layer_buckets.get(id(layer))
+            if keys is None:  # unknown module: be safe
+                keys = list(self._ag_events.keys())
+        stream = torch.cuda.current_stream(self.topology.device)
+        for k in keys:
+            ev = self._ag_events.pop(k, None)
+            if ev is not None:
+                stream.wait_event(ev)
+
+    def _gather_bucket(self, g: OptimizerParamGroup, gi: int, b: int) -> None:
+        full = g.bucket_view(g.flat_param, b)
+        mine = g.param_chunk_view(b)
+        if self._async_param_gather():
+            assert self._comm_stream is not None
+            self._comm_stream.wait_stream(torch.cuda.current_stream(self.topology.device))
+            with torch.cuda.stream(self._comm_stream):
+                dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
+                ev = torch.cuda.Event()
+                ev.record(self._comm_stream)
+            self._ag_events[(gi, b)] = ev
+        elif self._gpu:
+            dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
+        else:
+            parts = list(full.view(self.dp, g.chunk).unbind(0))
+            dist.all_gather(parts, mine.clone(), group=self.topology.data_parallel_group)
+
     def step(self) -> OptimizerStepOutput:
+        self.wait_param_sync()  # parameters never touched by a forward (frozen / unused) still must land
         self.step_index += 1
         for g in self.parameter_groups:
             g.set_dummy_grad()
@@ -236,8 +291,9 @@ class Optimizer(BaseOptimizer):
                     weight_decay=g.config.weight_decay, step=g.adam_step, grad_scale=gscale,
                     param_out=g.param_chunk_view(b),
                 )
+                if self.config.zero and self.dp > 1:
+                    self._gather_bucket(g, gi, b)
             learning_rates[g.config.name or f"parameter_group_{gi}"] = g.lr
-        self._refresh_params()
         self.zero_grad()
         return OptimizerStepOutput(global_grad_norm, None, learning_rates, ls_out.overflow, ls_out.no_overflow_steps,
                                    ls_out.current_loss_scale, debug_dict)
@@ -245,15 +301,10 @@ class Optimizer(BaseOptimizer):
     def _refresh_params(self) -> None:
         if not self.config.zero or self.dp == 1:
             return
-        for g in self.parameter_groups:
+        for gi, g in enumerate(self.parameter_groups):
             for b in range(g.num_buckets):
-                full = g.bucket_view(g.flat_param, b)
-                mine = g.param_chunk_view(b)
-                if self._gpu:
-                    dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
-                else:
-                    parts = list(full.view(self.dp, g.chunk).unbind(0))
-                    dist.all_gather(parts, mine.clone(), group=self.topology.data_parallel_group)
+                self._gather_bucket(g, gi, b)
+        self.wait_param_sync()
 
     def _debug_dict(self) -> dict[str, float]:
         d = {}
@@ -270,6 +321,7 @@ class Optimizer(BaseOptimizer):
         return self.config.gradient_clipping > 0.0 and global_grad_norm >= self.config.gradient_clipping
 
     def refresh_optimizer_after_model_change(self) -> None:
+        self.wait_param_sync()
         for g in self.parameter_groups:
             g.refresh_optimized_params(self.topology)
 
@@ -287,6 +339,7 @@ class Optimizer(BaseOptimizer):
         ]
 
     def state_dict(self) -> dict[str, Any]:
+        self.wait_param_sync()
         return {
             "step_index": self.step_index,
             "loss_scaler": self.loss_scaler.state_dict(),
@@ -333,6 +386,7 @@ class Optimizer(BaseOptimizer):
         return out
 
     def save_checkpoint(self, directory: Union[Path, str]) -> None:
+        self.wait_param_sync()
         directory = Path(directory)
         topo = self.topology
         if self.config.zero and self.config.zero_save_static:
@@ -371,6 +425,7 @@ class Optimizer(BaseOptimizer):
         logger.info("saved optimizer checkpoint")
 
     def load_checkpoint(self, directory: Union[Path, str]) -> None:
+        self.wait_param_sync()
         directory = Path(directory)
         topo = self.topology
         if self.config.zero and self.config.zero_save_static:

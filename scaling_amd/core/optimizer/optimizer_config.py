@@ -26,3 +26,8 @@ class OptimizerConfig(BaseConfig):
         "float32", description="dtype of the data-parallel gradient reduction ('float32' as the reference, or 'bfloat16')"
     )
     overlap_grad_reduce: bool = Field(True, description="overlap the data-parallel gradient reduction with backward")
+    overlap_param_gather: bool = Field(
+        True,
+        description="ZeRO: all-gather updated parameters bucket by bucket on a side stream and let each pipeline "
+        "layer's next forward wait only for its own buckets (overlaps the all-gather with the next step)",
+    )
