@@ -160,8 +160,10 @@ class PipePartitionedModule(torch.nn.Module):
         missing_dirs = [p for p in paths if not p.is_dir()]
         if missing_dirs:
             raise RuntimeError(f"Weight set directories missing: {missing_dirs}")
-        allowed_missing = list(allowed_missing_keys_in_checkpoint or [])
         ignore = list(ignore_keys_in_checkpoint or [])
+        # an ignored key keeps its initialisation: it is neither unexpected nor missing (the reference
+        # removes it from the file dict but would then report it missing)
+        allowed_missing = list(allowed_missing_keys_in_checkpoint or []) + ignore
         allowed_unexpected = list(allowed_unexpected_keys_in_checkpoint or []) + ignore
         missing, unexpected = set(), set()
         for li, layer in zip(self._global_layer_indices(), self._layers):

@@ -1,0 +1,204 @@
+"""End-to-end finetuning on CPU/gloo (reference: tests/transformer/test_finetuning.py): pretrain a tiny
+transformer on the reference's finetuning fixtures, then finetune only softprompt / adapter / BitFit bias /
+embedding-row parameters from the checkpoint and check that exactly those parameters move.
+
+Deviation: the reference's 128k tokenizer (``alpha-001-128k.json``) is not in the snapshot, so the LLaMA-2
+tokenizer fixture (vocab 32000) is used."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from tests.dist_utils import free_port
+
+pytestmark = pytest.mark.cpu
+ROOT = Path(__file__).resolve().parent.parent
+FILES = Path("/root/reference/tests/transformer/files")
+TOKENIZER = FILES / "llama2-tokenizer.json"
+needs_fixtures = pytest.mark.skipif(not (FILES / "dataset" / "finetuning.json").exists() or not TOKENIZER.exists(),
+                                    reason="reference fixtures not mounted")
+
+
+def _config(tmp: Path, mp: int, pp: int, world: int, mbs: int = 2, acc: int = 1, memory_map: bool = False,
+            data_prefixes=None, masked_softmax=None) -> dict:
+    if memory_map:
+        data = {"data_prefixes": [str(p) for p in (data_prefixes or [FILES / "dataset" / "finetuning_memory_map" / "dataset"])],
+                "blended_dataset": {"cache_directory": str(tmp)}, "finetuning_dataset": True,
+                "finetuning_dataset_memory_map": True}
+    else:
+        data = {"data_prefixes": [str(FILES / "dataset" / "finetuning.json")],
+                "blended_dataset": {"cache_directory": str(tmp)}, "finetuning_dataset": True}
+    # the memory-map fixture was tokenized with the reference's 128k vocabulary
+    vocab = 128000 if (memory_map and data_prefixes is None) else 32000
+    return {
+        "topology": {"world_size": world, "model_parallel_size": mp, "pipe_parallel_size": pp, "micro_batch_size": mbs,
+                     "gradient_accumulation_steps": acc},
+        "optimizer": {"beta1": 0.9, "beta2": 0.99, "gradient_clipping": 1.0,
+                      "loss_scaler": {"enable": False, "initial_scale": 16}, "zero": True},
+        "learning_rate_scheduler": {"learning_rate": 0.01, "learning_rate_minimum": 0.0,
+                                    "learning_rate_decay_style": "cosine", "learning_rate_warmup_steps": 2,
+                                    "learning_rate_decay_iters": 10},
+        "trainer": {"save_dir": str(tmp / "ckpt"), "save_interval": 6, "load_dir": str(tmp / "ckpt"),
+                    "train_iterations": 10, "assert_checkpoint_loaded": False},
+        "training": {"parameters_exclude": []},
+        "logger": {"log_level": "warning", "log_dir": str(tmp / "logs")},
+        "data": data,
+        "transformer_architecture": {
+            "weight_tying": False, "vocab_size": vocab, "vocab_file": str(TOKENIZER), "sequence_length": 64,
+            "hidden_size": 32, "num_attention_heads": 2, "num_layers": 2, "precision": "bfloat16",
+            "dropout_embedding": 0.1, "dropout_attention_probs": 0.1, "dropout_after_attention": 0.1,
+            "dropout_after_mlp": 0.1, "masked_softmax": masked_softmax or {"kernel": "torch"},
+        },
+    }
+
+
+def _run(tmp: Path, cfg: dict, world: int, tag: str) -> list:
+    spec = tmp / f"{tag}.json"
+    out = tmp / f"{tag}.out.json"
+    spec.write_text(json.dumps({"config": cfg, "out": str(out)}))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(ROOT / "tests" / "train_helper.py"),
+           str(spec)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
+    assert r.returncode == 0, r.stderr[-5000:]
+    return json.loads(out.read_text())
+
+
+def _load_full(file: Path) -> dict:
+    sd: dict = {}
+    for f in file.parent.glob(f"{file.stem}*.pt"):
+        sd.update(torch.load(str(f), map_location="cpu", weights_only=True))
+    return sd
+
+
+def _finetune_config(cfg: dict) -> dict:
+    cfg["trainer"].update(assert_checkpoint_loaded=True, load_optimizer_states=False, load_context=False,
+                          save_interval=2, train_iterations=4)
+    cfg["training"]["finetune"] = True
+    cfg["training"]["finetunable_parameters"] = ["finetuning"]
+    return cfg
+
+
+def _compare(tmp: Path, marker: str, skip_suffix=None, layer_filter=None) -> int:
+    ck = tmp / "ckpt"
+    baseline_dir = ck / "global_step6"
+    found = 0
+    for f in baseline_dir.glob("model_state*.pt"):
+        base = torch.load(str(f), map_location="cpu", weights_only=True)
+        s2 = _load_full(ck / "global_step2" / f.name)
+        s4 = _load_full(ck / "global_step4" / f.name)
+        new = [k for k in s2 if marker in k]
+        if layer_filter is None or layer_filter in f.name:
+            for k in new:
+                assert (s2[k] != s4[k]).any(), f"parameter {k} was not trained ({f.name})"
+            found += len(new)
+        for k in base:
+            if skip_suffix and k.endswith(skip_suffix):
+                continue
+            assert torch.equal(base[k], s2[k]), f"frozen parameter {k} changed ({f.name})"
+    return found
+
+
+@needs_fixtures
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (1, 2, 2), (2, 1, 2)])
+def test_softprompt_finetuning(tmp_path, mp, pp, world):
+    cfg = _config(tmp_path, mp, pp, world)
+    _run(tmp_path, cfg, world, "pre")
+    cfg = _finetune_config(cfg)
+    cfg["trainer"]["allowed_missing_keys_in_checkpoint"] = ["softprompt_finetuning"]
+    cfg["transformer_architecture"]["softprompt_config"] = {"name": "finetuning", "n_tokens": 8}
+    _run(tmp_path, cfg, world, "ft")
+    assert _compare(tmp_path, "softprompt_finetuning") > 0
+
+
+@needs_fixtures
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (2, 1, 2)])
+@pytest.mark.parametrize("kernel", ["torch", "flash_attention"])
+def test_adapter_finetuning(tmp_path, mp, pp, world, kernel):
+    cfg = _config(tmp_path, mp, pp, world, masked_softmax={"kernel": kernel})
+    _run(tmp_path, cfg, world, "pre")
+    cfg = _finetune_config(cfg)
+    cfg["trainer"]["allowed_missing_keys_in_checkpoint"] = [
+        "attn_adapter_finetuning.dense_in.weight", "attn_adapter_finetuning.dense_out.weight",
+        "mlp_adapter_finetuning.dense_in.weight", "mlp_adapter_finetuning.dense_out.weight"]
+    cfg["transformer_architecture"]["adapter_config"] = {"name": "finetuning", "attention_downsampling_factor": 0.25,
+                                                         "mlp_downsampling_factor": 0.25, "init_std": 0.1}
+    _run(tmp_path, cfg, world, "ft")
+    assert _compare(tmp_path, "adapter_finetuning", layer_filter="TransformerLayer") > 0
+
+
+@needs_fixtures
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (1, 2, 2)])
+@pytest.mark.parametrize("memory_map", [False, True])
+def test_bitfit_finetuning(tmp_path, mp, pp, world, memory_map):
+    cfg = _config(tmp_path, mp, pp, world, memory_map=memory_map)
+    _run(tmp_path, cfg, world, "pre")
+    cfg = _finetune_config(cfg)
+    cfg["transformer_architecture"]["bitfit_bias_config"] = {"name": "finetuning"}
+    cfg["trainer"]["allowed_missing_keys_in_checkpoint"] = ["finetuning"]
+    cfg["trainer"]["allowed_unexpected_keys_in_checkpoint"] = ["bias"]
+    _run(tmp_path, cfg, world, "ft")
+    assert _compare(tmp_path, "bias_finetuning", skip_suffix=".bias", layer_filter="TransformerLayer") > 0
+
+
+@needs_fixtures
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (2, 1, 2)])
+def test_finetuning_with_ignore_keys_in_checkpoint(tmp_path, mp, pp, world):
+    cfg = _config(tmp_path, mp, pp, world, acc=2)
+    _run(tmp_path, cfg, world, "pre")
+    cfg = _finetune_config(cfg)
+    cfg["training"]["finetunable_parameters"] = ["embedding.weight"]
+    cfg["trainer"]["ignore_keys_in_checkpoint"] = ["embedding.weight"]
+    losses = _run(tmp_path, cfg, world, "ft")
+    assert len(losses) == 4 and all(np.isfinite(m["training/loss"]) for m in losses)
+
+
+@needs_fixtures
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (1, 2, 2)])
+@pytest.mark.parametrize("finetunable", [["embedding.weight"], ["embedding.weight", "mlp.dense_in.weight"]])
+def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
+    """Only the rows of ``finetunable_token_ids`` of the (tied) embedding may change."""
+    sys.path.insert(0, str(ROOT))
+    from scaling_amd.core import MemoryMapDatasetBuilder
+    from scaling_amd.transformer.tokenizer import Tokenizer
+
+    prefix = tmp_path / "emb" / "tokens"
+    tok = Tokenizer.from_file(str(TOKENIZER))
+    ids = tok.encode("Abra kadabra zweimal schwarzer Kater") + [tok.eos_token_id]
+    rows = [0, 77, 222, 31995]
+    ids += list(range(4)) + rows + [tok.eos_token_id]
+    with MemoryMapDatasetBuilder(prefix) as b:
+        for _ in range(10):
+            b.add(np.array(ids))
+    cfg = _config(tmp_path, mp, pp, world, mbs=1, memory_map=True, data_prefixes=[prefix])
+    cfg["training"]["finetune"] = True
+    cfg["transformer_architecture"]["weight_tying"] = True
+    cfg["transformer_architecture"]["finetunable_token_ids"] = rows
+    cfg["training"]["finetunable_parameters"] = finetunable
+    _run(tmp_path, cfg, world, "pre")
+    cfg["trainer"].update(save_interval=2, train_iterations=4, assert_checkpoint_loaded=True,
+                          load_optimizer_states=False, load_context=False)
+    _run(tmp_path, cfg, world, "ft")
+    ck = tmp_path / "ckpt"
+    reached = [False, False]
+    for f in (ck / "global_step6").glob("model_state*.pt"):
+        if "EmbeddingInput" not in f.name and "LMHead" not in f.name:
+            continue
+        s2, s4 = _load_full(ck / "global_step2" / f.name), _load_full(ck / "global_step4" / f.name)
+        for name in finetunable:
+            if name not in s2:
+                continue
+            for tid, (a, b) in enumerate(zip(s2[name], s4[name])):
+                if tid in rows:
+                    reached[0] = True
+                    assert not torch.equal(a, b), f"row {tid} not trained"
+                else:
+                    reached[1] = True
+                    assert torch.equal(a, b), f"row {tid} changed"
+    assert all(reached)
