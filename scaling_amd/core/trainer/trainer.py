@@ -12,6 +12,7 @@ from typing import Any, Callable, Generic, Optional, TypeVar
 
 import torch
 
+from ..utils.watchdog import HangWatchdog
 from ..context import BaseContext, DeterminedBaseContext
 from ..data import BaseDataset, DataLoader
 from ..logging import logger
@@ -183,20 +184,34 @@ class BaseTrainer(Generic[BaseContextGeneric, ParallelModuleGeneric]):
         logger.log_metrics(metrics, step=self.context.iterations)
         return metrics
 
+    def _start_watchdog(self) -> Optional[HangWatchdog]:
+        if not self.config.hang_watchdog_seconds:
+            return None
+        log_dir = getattr(getattr(self.context.config, "logger", None), "log_dir", None)
+        return HangWatchdog(self.config.hang_watchdog_seconds, rank=self.context.topology.config.global_rank,
+                            log_dir=log_dir, abort=self.config.hang_watchdog_abort)
+
     def run_training(self, return_metrics: bool = False) -> Optional[list[dict[str, Any]]]:
         out: list[dict[str, Any]] = []
-        while self.context.iterations < (self.config.train_iterations or 0):
-            tso = self.train_step()
-            if (self.config.save_interval is not None and self.config.save_dir is not None
-                    and self.context.iterations % self.config.save_interval == 0):
-                self.save_checkpoint()
-            eso = None
-            if self.config.eval_interval is not None and self.context.iterations % self.config.eval_interval == 0:
-                eso = self.eval_step()
-            if self.context.topology.config.global_rank == 0:
-                m = self.log_metrics(tso, eso)
-                if return_metrics:
-                    out.append(m)
+        watchdog = self._start_watchdog()
+        try:
+            while self.context.iterations < (self.config.train_iterations or 0):
+                tso = self.train_step()
+                if (self.config.save_interval is not None and self.config.save_dir is not None
+                        and self.context.iterations % self.config.save_interval == 0):
+                    self.save_checkpoint()
+                eso = None
+                if self.config.eval_interval is not None and self.context.iterations % self.config.eval_interval == 0:
+                    eso = self.eval_step()
+                if self.context.topology.config.global_rank == 0:
+                    m = self.log_metrics(tso, eso)
+                    if return_metrics:
+                        out.append(m)
+                if watchdog is not None:
+                    watchdog.heartbeat()
+        finally:
+            if watchdog is not None:
+                watchdog.stop()
         return out if return_metrics else None
 
 

@@ -27,6 +27,11 @@ class TrainerConfig(BaseConfig):
     dataloader_prefetch_factor: Optional[int] = Field(None, description="")
     eval_iterations: int = Field(1, description="(not implemented in the reference either: one eval step)")
     eval_interval: Optional[int] = Field(None, description="evaluate every eval_interval steps")
+    hang_watchdog_seconds: Optional[float] = Field(
+        None, description="MI355X addition: dump all thread stacks when a train step makes no progress for this many "
+        "seconds (RCCL hang / stuck kernel diagnosis); None disables"
+    )
+    hang_watchdog_abort: bool = Field(False, description="exit the rank (code 124) after the hang dump so the launcher fails fast")
     separate_file_for_parameters: Optional[list[str]] = Field(
         None, description="create a separate checkpoint file for parameters matching these names"
     )

@@ -286,3 +286,22 @@ def test_parameter_count_independent_of_layout(mp, pp):
     other = run_distributed(_param_count_body, world_size=2, mp=mp, pp=pp)
     for r in other.values():
         assert r[1] == base[1]
+
+
+# ---------------------------------------------------------------- hang watchdog
+def test_hang_watchdog_dumps_stacks_on_stall(tmp_path):
+    import time
+
+    from scaling_amd.core.utils.watchdog import HangWatchdog
+
+    seen = []
+    wd = HangWatchdog(0.3, rank=3, log_dir=tmp_path, on_hang=seen.append, poll_s=0.05)
+    for _ in range(5):  # steady heartbeats: no report
+        time.sleep(0.05)
+        wd.heartbeat()
+    assert wd.fired == 0
+    time.sleep(0.6)  # stall
+    wd.stop()
+    assert wd.fired >= 1 and seen and seen[0] >= 0.3
+    dump = (tmp_path / "hang_rank3.txt").read_text()
+    assert "no progress" in dump and "test_hang_watchdog_dumps_stacks_on_stall" in dump
