@@ -92,7 +92,7 @@ class PDSHRunner:
         return ["pdsh", "-S", "-f", "1024", "-w", ",".join(self.pool.keys()), f"cd {os.getcwd()}; {exports} {inner}"]
 
 
-def runner_main(config: RunnerConfig, payload: Optional[dict[str, Any]] = None) -> None:
+def runner_main(config: RunnerConfig, payload: Optional[dict[str, Any]] = None) -> int:
     pool = get_resource_pool(config)
     hosts = list(pool.keys())
     if config.master_addr is not None:
@@ -107,5 +107,6 @@ def runner_main(config: RunnerConfig, payload: Optional[dict[str, Any]] = None) 
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     proc = subprocess.Popen(cmd, env=env)
     rc = proc.wait()
-    if rc != 0:
+    if rc != 0:  # the failing rank already printed its error; propagate the code quietly
         sys.exit(rc)
+    return rc
