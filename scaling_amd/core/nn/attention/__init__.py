@@ -1,4 +1,5 @@
 from .attention import (
+    KVCache,
     ParallelSelfAttention,
     RelativePositionEmbeddingType,
     cumulative_seq_lengths_to_dense_attention_mask,
@@ -9,6 +10,7 @@ from .attention import (
 )
 
 __all__ = [
+    "KVCache",
     "ParallelSelfAttention",
     "RelativePositionEmbeddingType",
     "cumulative_seq_lengths_to_dense_attention_mask",

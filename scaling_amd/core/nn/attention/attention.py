@@ -124,6 +124,43 @@ def multi_head_attention(
     return out.transpose(1, 2).reshape(b, sq, n * hd)
 
 
+class KVCache:
+    """Preallocated, token-major decode cache ``[capacity, nkv, hd]`` for keys and values.
+
+    The reference grows its cache with one ``torch.cat`` per generated token
+    (``src/scaling/core/nn/attention/attention.py:580-588``), which copies the whole history every
+    step (O(n^2) HBM traffic over a generation).  Here the buffers are allocated once with headroom
+    and doubled when full, so a decode step writes only its new rows; ``append`` returns views of
+    the valid prefix, which the flash kernel reads directly (bottom-right causal alignment).
+    """
+
+    def __init__(self, k: torch.Tensor, v: torch.Tensor, length: int) -> None:
+        self.k, self.v, self.length = k, v, length
+
+    @classmethod
+    def start(cls, k: torch.Tensor, v: torch.Tensor, headroom: int = 256) -> "KVCache":
+        n = k.shape[0]
+        kb = k.new_empty((n + headroom,) + tuple(k.shape[1:]))
+        vb = v.new_empty((n + headroom,) + tuple(v.shape[1:]))
+        kb[:n].copy_(k)
+        vb[:n].copy_(v)
+        return cls(kb, vb, n)
+
+    def append(self, k: torch.Tensor, v: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        n, m = self.length, k.shape[0]
+        if n + m > self.k.shape[0]:
+            cap = max(2 * self.k.shape[0], n + m)
+            kb = self.k.new_empty((cap,) + tuple(self.k.shape[1:]))
+            vb = self.v.new_empty((cap,) + tuple(self.v.shape[1:]))
+            kb[:n].copy_(self.k[:n])
+            vb[:n].copy_(self.v[:n])
+            self.k, self.v = kb, vb
+        self.k[n : n + m].copy_(k)
+        self.v[n : n + m].copy_(v)
+        self.length = n + m
+        return self.k[: self.length], self.v[: self.length]
+
+
 class ParallelSelfAttention(torch.nn.Module):
     def __init__(
         self,
@@ -239,7 +276,7 @@ class ParallelSelfAttention(torch.nn.Module):
             parallel_output=(topology.config.sequence_parallel if topology is not None else False),
         )
         self.masked_softmax = MaskedSoftmax(config=masked_softmax_config)
-        self.cache: dict[int, tuple[Optional[torch.Tensor], Optional[torch.Tensor]]] = {}
+        self.cache: dict[int, Union["KVCache", tuple[None, None]]] = {}
 
     # ------------------------------------------------------------------ projections
     def _project(self, x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -334,13 +371,11 @@ class ParallelSelfAttention(torch.nn.Module):
                 raise ValueError("KV caching is only supported for causal attention.")
             assert b == 1, f"KV caching is only supported for batch size 1, got {b}"
             if reset_cache:
-                self.cache[cache_index] = (k, v)
+                self.cache[cache_index] = KVCache.start(k, v)
             else:
-                pk, pv = self.cache[cache_index]
-                assert pk is not None and pv is not None
-                k = torch.cat((pk, k), dim=0)
-                v = torch.cat((pv, v), dim=0)
-                self.cache[cache_index] = (k, v)
+                kv = self.cache[cache_index]
+                assert isinstance(kv, KVCache), "use_cache without a preceding reset_cache"
+                k, v = kv.append(k, v)
             cumulative_seq_lengths_key = torch.tensor([0, k.shape[0]], device=x.device, dtype=torch.int32)
         elif reset_cache:
             self.cache[cache_index] = (None, None)

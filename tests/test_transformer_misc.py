@@ -130,3 +130,22 @@ def test_mlp_example_trains(tmp_path):
                        capture_output=True, text=True, timeout=600, env=dict(os.environ, PYTHONPATH=str(ROOT)))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "completed step 30" in r.stdout + r.stderr
+
+
+def test_kv_cache_preallocated_growth():
+    """The decode cache appends in place and doubles capacity only when full (no per-token concat)."""
+    from scaling_amd.core.nn.attention import KVCache
+
+    k0, v0 = torch.randn(5, 2, 4), torch.randn(5, 2, 4)
+    c = KVCache.start(k0, v0, headroom=3)
+    ref_k, ref_v = [k0], [v0]
+    buf = c.k
+    for i in range(10):
+        k1, v1 = torch.randn(1, 2, 4), torch.randn(1, 2, 4)
+        ref_k.append(k1)
+        ref_v.append(v1)
+        k, v = c.append(k1, v1)
+        if i < 3:
+            assert c.k is buf  # filled in place while capacity lasts
+        assert torch.equal(k, torch.cat(ref_k)) and torch.equal(v, torch.cat(ref_v))
+    assert c.length == 15 and c.k.shape[0] >= 15
