@@ -47,8 +47,6 @@ def _args() -> argparse.Namespace:
                    help="hipBLASLt solution table (scaling_amd/tuning/gemm_gfx950.csv); tune = benchmark and write")
     p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
-    p.add_argument("--share-gpu", action="store_true",
-                   help="rehearsal only: map local ranks onto the visible GPUs round-robin (several ranks per GPU)")
     return p.parse_args()
 
 
@@ -86,10 +84,6 @@ def main() -> None:
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local = _env_int("LOCAL_RANK", 0)
-    if a.share_gpu:
-        import torch.cuda as _tc
-
-        local = local % max(1, _tc.device_count())
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
