@@ -22,48 +22,21 @@
 #include <string>
 #include <vector>
 
+#include "data_index_core.h"
+
 namespace py = pybind11;
 
 namespace {
 
-struct Entry {
-    int64_t sampled, target;
-    int64_t ds;
-};
-// "a has lower priority than b" for std::priority_queue (max-heap) => we want min ratio first.
-struct Worse {
-    bool operator()(const Entry& a, const Entry& b) const {
-        // ratio a = a.sampled / a.target ; compare a > b  (so smaller ratio pops first)
-        const __int128 l = (__int128)a.sampled * b.target, r = (__int128)b.sampled * a.target;
-        if (l != r) return l > r;
-        return a.ds > b.ds;  // tie: lower dataset index first
-    }
-};
-
 int64_t blended_sample(py::array_t<int64_t, py::array::c_style | py::array::forcecast> counts, const std::string& stem) {
     auto c = counts.unchecked<1>();
     const int64_t n = c.shape(0);
-    if (n <= 0) throw std::invalid_argument("blended_sample: need at least one dataset");
-    int64_t total = 0;
-    std::priority_queue<Entry, std::vector<Entry>, Worse> pq;
-    for (int64_t i = 0; i < n; ++i) {
-        if (c(i) <= 0) throw std::invalid_argument("blended_sample: counts must be positive");
-        total += c(i);
-        pq.push({0, c(i), i});
-    }
     std::vector<int64_t> out;
-    out.reserve((size_t)total * 2);
     {
         py::gil_scoped_release nogil;
-        while (!pq.empty()) {
-            Entry e = pq.top();
-            pq.pop();
-            out.push_back(e.ds);
-            out.push_back(e.sampled);
-            e.sampled += 1;
-            if (e.sampled < e.target) pq.push(e);
-        }
+        out = scaling_data::blended_order(counts.data(), n);
     }
+    const int64_t total = (int64_t)out.size() / 2;
     {
         std::ofstream f(stem + ".bin", std::ios::binary);
         f.write(reinterpret_cast<const char*>(out.data()), (std::streamsize)(out.size() * sizeof(int64_t)));
@@ -89,50 +62,11 @@ int64_t blended_sample(py::array_t<int64_t, py::array::c_style | py::array::forc
 py::tuple text_index(py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_sizes,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_order, int64_t seq_len,
                      bool only_full_sequences, int64_t allow_incomplete_every_n) {
-    auto sz = doc_sizes.unchecked<1>();
-    auto order = doc_order.unchecked<1>();
     std::vector<int64_t> data, index;
     {
         py::gil_scoped_release nogil;
-        std::vector<int64_t> item;
-        int64_t item_tokens = 0, full = 0, half = 0, pos_total = 0;
-        bool in_half = false;
-        for (int64_t oi = 0; oi < order.shape(0); ++oi) {
-            const int64_t doc = order(oi);
-            const int64_t count = sz(doc);
-            int64_t pos = 0;
-            while (pos < count - 1) {
-                const int64_t end = std::min(count, pos + 1 + seq_len - item_tokens);
-                if (only_full_sequences) {
-                    if (in_half) {
-                    } else if (end - pos < seq_len + 1) {
-                        if (allow_incomplete_every_n != 0 &&
-                            ((double)full / (double)allow_incomplete_every_n - (double)half) >= 1.0) {
-                            in_half = true;
-                        } else {
-                            break;
-                        }
-                    } else {
-                        full += 1;
-                    }
-                }
-                item_tokens += end - pos;
-                item.push_back(doc);
-                item.push_back(pos);
-                item.push_back(end);
-                if (item_tokens == seq_len + 1) {
-                    index.push_back(pos_total);
-                    index.push_back((int64_t)item.size());
-                    pos_total += (int64_t)item.size();
-                    data.insert(data.end(), item.begin(), item.end());
-                    item.clear();
-                    item_tokens = 0;
-                    if (in_half) half += 1;
-                    in_half = false;
-                }
-                pos = end - 1;
-            }
-        }
+        scaling_data::text_index(doc_sizes.data(), doc_sizes.shape(0), doc_order.data(), doc_order.shape(0), seq_len,
+                                 only_full_sequences, allow_incomplete_every_n, data, index);
     }
     py::array_t<int64_t> d((py::ssize_t)data.size()), ix((py::ssize_t)index.size());
     std::copy(data.begin(), data.end(), d.mutable_data());
