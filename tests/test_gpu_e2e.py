@@ -133,3 +133,28 @@ def test_gpu_training_resume_bit_exact(tmp_path, dropout, kernel):
     cfg["trainer"]["assert_checkpoint_loaded"] = True
     resumed = _train(tmp_path, cfg, "resumed")
     assert resumed == full[-4:], (full, resumed)
+
+
+@pytest.mark.parametrize("kernel", ["flash_attention", "torch"])
+def test_gpu_cached_generation_matches_uncached(kernel):
+    """Decode with the preallocated KV cache (flash kernel, bottom-right causal alignment for s_q=1) against
+    full recomputation each step (reference: tests/transformer/test_inference.py, cached vs uncached)."""
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+    from scaling_amd.transformer.inference import TransformerInferenceModule
+    from scaling_amd.transformer.model.model import get_transformer_layer_specs
+
+    arch = TransformerArchitectureConfig(
+        vocab_size=256, hidden_size=256, num_layers=2, num_attention_heads=4, sequence_length=128, norm_type="rms",
+        mlp_type="swiglu", mlp_factor=2.0, precision="bfloat16", attention_num_kv_heads=2, attention_qkv_in_one=False,
+        relative_position_embedding_type="rotary_complex", masked_softmax={"kernel": kernel})
+    torch.manual_seed(0)
+    m = TransformerInferenceModule(get_transformer_layer_specs(arch), devices=(0,))
+    prompt = [3, 17, 42, 99, 5, 7, 11]
+    a = m.generate(12, input_tokens=prompt, stop_tokens=[], use_cache=True)
+    b = m.generate(12, input_tokens=prompt, stop_tokens=[], use_cache=False)
+    n = 0
+    while n < min(len(a.completion_tokens), len(b.completion_tokens)) and a.completion_tokens[n] == b.completion_tokens[n]:
+        n += 1
+    assert n >= 1, (a.completion_tokens, b.completion_tokens)
+    la, lb = a.completion_logits[:n].float().cpu(), b.completion_logits[:n].float().cpu()
+    torch.testing.assert_close(la, lb, rtol=5e-2, atol=5e-2)
