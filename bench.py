@@ -1,6 +1,6 @@
 """Headline benchmark: whole-node training tokens/s of the Llama-2-7B shape in bf16 (BASELINE.json).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W            # self-launches N ranks (one per GPU)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -10,24 +10,35 @@ last backward, grad-norm clipping and the fused ZeRO-1 AdamW update + parameter 
 synthetic token ids of the benchmark shape, weights are random-init.  Per-GPU work is fixed (weak
 scaling): every data-parallel rank processes ``micro_batch * grad_acc`` sequences per step.
 
-Rank 0 prints one JSON line; ``value`` is the whole-job tokens/s (global tokens / max-over-ranks step time).
+Launch: without ``WORLD_SIZE`` in the environment and ``--gpus N > 1`` this process becomes a launcher
+(reference ``core/runner/launch.py:73-161``): it spawns N worker processes of itself with
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, never touches the GPU, kills the siblings as soon as one rank
+fails and exits with that rank's code.
+
+Rank 0 prints one JSON line; ``value`` is the whole-job tokens/s (global tokens / max-over-ranks time).
+The line also carries what the ranks saw: the world size of the process group, every rank's step time,
+and whether the parameters of all data-parallel replicas agree bit-for-bit after the last step.
+
+``--backend gloo`` runs the same path on CPU processes (plumbing mode for the CPU test-suite).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 from typing import Any, Optional
 
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+METRIC = "tokens/sec (whole node) Llama-2-7B-shape bf16, TP×PP×DP on 1/2/4/8 MI355X"
 
-def _args() -> argparse.Namespace:
+
+def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -42,12 +53,19 @@ def _args() -> argparse.Namespace:
                    choices=["disabled", "every_layer", "every_pipe_stage"])
     p.add_argument("--sequence-parallel", action="store_true")
     p.add_argument("--zero", type=int, default=1)
+    p.add_argument("--lora", action="store_true",
+                   help="LoRA finetune path (BASELINE #5): q/k/v/dense adapters trained, base weights frozen")
+    p.add_argument("--lora-rank", type=int, default=64)
+    p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo"],
+                   help="gloo = CPU processes (plumbing mode, no GPU)")
+    p.add_argument("--precision", type=str, default="bfloat16", choices=["bfloat16", "float32"])
     p.add_argument("--num-layers", type=int, default=None, help="debug only: marks the result as not the headline config")
     p.add_argument("--gemm-tuning", type=str, default="use", choices=["use", "tune", "off"],
                    help="hipBLASLt solution table (scaling_amd/tuning/gemm_gfx950.csv); tune = benchmark and write")
     p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
-    return p.parse_args()
+    p.add_argument("--launch-timeout", type=float, default=3000.0, help="launcher: kill all ranks after this many s")
+    return p.parse_args(argv)
 
 
 def _env_int(k: str, d: int) -> int:
@@ -55,19 +73,78 @@ def _env_int(k: str, d: int) -> int:
     return d if v is None else int(v)
 
 
+# ---------------------------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def _launch(a: argparse.Namespace) -> int:
+    """Spawns one worker per GPU (this file, with the rank env set); fail-fast on the first bad exit."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs: list[subprocess.Popen] = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if a.backend == "gloo":  # CPU ranks: do not oversubscribe the host's cores
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // a.gpus)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+    def _kill_all(sig: int) -> None:
+        for q in procs:
+            if q.poll() is None:
+                try:
+                    q.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    def _on_signal(signum: int, _frame: Any) -> None:
+        _kill_all(signum)
+
+    signal.signal(signal.SIGTERM, _on_signal)
+    signal.signal(signal.SIGINT, _on_signal)
+    deadline = time.time() + a.launch_timeout
+    rc = 0
+    while True:
+        codes = [q.poll() for q in procs]
+        bad = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            i, rc = bad[0]
+            print(f"bench launcher: rank {i} exited with {rc}; terminating the other ranks", file=sys.stderr, flush=True)
+            break
+        if all(c == 0 for c in codes):
+            return 0
+        if time.time() > deadline:
+            print("bench launcher: timeout, terminating all ranks", file=sys.stderr, flush=True)
+            rc = 124
+            break
+        time.sleep(0.2)
+    _kill_all(signal.SIGTERM)
+    t_end = time.time() + 20
+    while time.time() < t_end and any(q.poll() is None for q in procs):
+        time.sleep(0.2)
+    _kill_all(signal.SIGKILL)
+    for q in procs:
+        q.wait()
+    return rc if rc > 0 else 1
+
+
+# ---------------------------------------------------------------------------------------------- worker
 class _SyntheticLoader:
     """Infinite iterator of fixed random token batches (generated once per slot, on host)."""
 
-    def __init__(self, micro_batch: int, seq_len: int, vocab: int, seed: int, slots: int = 4):
+    def __init__(self, micro_batch: int, seq_len: int, vocab: int, seed: int, pin: bool, slots: int = 4):
+        import torch
+
         from scaling_amd.transformer.data.text_dataset_batch import TextDatasetBatchBeforeSync
 
         g = torch.Generator().manual_seed(seed)
-        self.batches = [
-            TextDatasetBatchBeforeSync(token_ids=torch.randint(1, vocab, (micro_batch, seq_len + 1), generator=g).pin_memory()
-                                       if torch.cuda.is_available() else
-                                       torch.randint(1, vocab, (micro_batch, seq_len + 1), generator=g))
-            for _ in range(slots)
-        ]
+        self.batches = []
+        for _ in range(slots):
+            ids = torch.randint(1, vocab, (micro_batch, seq_len + 1), generator=g)
+            self.batches.append(TextDatasetBatchBeforeSync(token_ids=ids.pin_memory() if pin else ids))
         self.i = 0
 
     def __iter__(self) -> "_SyntheticLoader":
@@ -79,56 +156,97 @@ class _SyntheticLoader:
         return b
 
 
-def main() -> None:
-    a = _args()
+def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> dict[str, Any]:
+    from scaling_amd.models import llama_architecture
+
+    dp = world // (a.tp * a.pp)
+    arch = llama_architecture(a.model, sequence_length=a.seq_len, precision=a.precision)
+    if a.num_layers is not None:
+        arch["num_layers"] = a.num_layers
+    training: dict[str, Any] = {"weight_decay": 0.1}
+    if a.lora:
+        arch["lora_config"] = {"name": "lora", "rank": a.lora_rank, "alpha": 16,
+                               "parallel_modules": ["query", "key", "value", "dense"]}
+        training.update(finetune=True, finetunable_parameters=["lora"])
+    topo: dict[str, Any] = {
+        "world_size": world, "global_rank": rank, "local_slot": local,
+        "model_parallel_size": a.tp, "pipe_parallel_size": a.pp, "data_parallel_size": dp,
+        "micro_batch_size": a.micro_batch, "gradient_accumulation_steps": a.grad_acc,
+        "activation_checkpointing_type": a.activation_checkpointing, "sequence_parallel": a.sequence_parallel,
+    }
+    if a.backend == "gloo":
+        topo["backend"] = "gloo"
+    return {
+        "topology": topo,
+        "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero)},
+        "learning_rate_scheduler": {"learning_rate": 3e-4, "learning_rate_minimum": 3e-5,
+                                    "learning_rate_decay_style": "cosine", "learning_rate_warmup_steps": 2,
+                                    "learning_rate_decay_iters": 1000},
+        "training": training,
+        "trainer": {"seed": 42, "train_iterations": a.warmup + a.steps},
+        "logger": {"log_level": "warning"},
+        "transformer_architecture": arch,
+    }
+
+
+def _param_checksum(model: Any, device: Any) -> Any:
+    """(sum, sum of squares, index-weighted sum) over this rank's parameters, in float64."""
+    import torch
+
+    acc = torch.zeros(3, dtype=torch.float64, device=device)
+    with torch.no_grad():
+        for i, p in enumerate(model.parameters()):
+            x = p.detach().double()
+            acc[0] += x.sum()
+            acc[1] += (x * x).sum()
+            acc[2] += (i + 1) * x.sum()
+    return acc
+
+
+def _worker(a: argparse.Namespace) -> None:
+    import torch
+    import torch.distributed as dist
+
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local = _env_int("LOCAL_RANK", 0)
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29611")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()) if world == 1 else "29611")
     assert world % (a.tp * a.pp) == 0, "world size must be divisible by tp*pp"
     dp = world // (a.tp * a.pp)
 
     from scaling_amd.core import Topology
     from scaling_amd.core.logging import LoggerConfig, logger
-    from scaling_amd.models import llama_architecture
     from scaling_amd.transformer.context import TransformerConfig, TransformerContext
     from scaling_amd.transformer.data.text_dataset import TextDataset
     from scaling_amd.transformer.model import init_model, init_optimizer
     from scaling_amd.transformer.model.model import loss_function, metrics_aggregation_fn
-
     from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
 
-    gemm_mode = enable_tuned_gemms(a.gemm_tuning, a.gemm_tuning_out, rank)
-    arch = llama_architecture(a.model, sequence_length=a.seq_len)
-    if a.num_layers is not None:
-        arch["num_layers"] = a.num_layers
-    cfg_dict = {
-        "topology": {
-            "world_size": world, "global_rank": rank, "local_slot": local,
-            "model_parallel_size": a.tp, "pipe_parallel_size": a.pp, "data_parallel_size": dp,
-            "micro_batch_size": a.micro_batch, "gradient_accumulation_steps": a.grad_acc,
-            "activation_checkpointing_type": a.activation_checkpointing, "sequence_parallel": a.sequence_parallel,
-        },
-        "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero)},
-        "learning_rate_scheduler": {"learning_rate": 3e-4, "learning_rate_minimum": 3e-5,
-                                    "learning_rate_decay_style": "cosine", "learning_rate_warmup_steps": 2,
-                                    "learning_rate_decay_iters": 1000},
-        "training": {"weight_decay": 0.1},
-        "trainer": {"seed": 42, "train_iterations": a.warmup + a.steps},
-        "logger": {"log_level": "warning"},
-        "transformer_architecture": arch,
-    }
+    gpu = a.backend != "gloo"
+    gemm_mode = enable_tuned_gemms(a.gemm_tuning, a.gemm_tuning_out, rank) if gpu else "off"
+    cfg_dict = _config_dict(a, world, rank, local)
+    arch = cfg_dict["transformer_architecture"]
     config = TransformerConfig.from_dict(cfg_dict)
     logger.configure(LoggerConfig(log_level="warning"), name=f"RANK {rank}", global_rank=rank)
     topology = Topology(config=config.topology)
     context = TransformerContext(config=config, topology=topology)
     context.initialize(master_addr=os.environ["MASTER_ADDR"], master_port=os.environ["MASTER_PORT"], seed=42)
+    dev = topology.device
+    if gpu and dev.type != "cuda":
+        raise SystemExit("bench.py: no GPU visible (use --backend gloo for the CPU plumbing mode)")
+    if os.environ.get("BENCH_FAIL_RANK") == str(rank):  # launcher fail-fast test hook
+        raise SystemExit(3)
     model = init_model(context=context)
     optimizer = init_optimizer(context=context, model=model)
-    loader = _SyntheticLoader(a.micro_batch, a.seq_len, arch["vocab_size"], seed=1234 + topology.data_parallel_rank)
+    loader = _SyntheticLoader(a.micro_batch, a.seq_len, arch["vocab_size"], seed=1234 + topology.data_parallel_rank,
+                              pin=gpu)
+
+    def sync() -> None:
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
 
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,
@@ -138,9 +256,8 @@ def main() -> None:
 
     for _ in range(a.warmup):
         step()
-    dev = topology.device
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     per_step = []
     last: Optional[Any] = None
@@ -149,17 +266,38 @@ def main() -> None:
         last = step()
         per_step.append(time.perf_counter() - s0)
     dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    sec = float(elapsed.item())
+    sync()
+    mine = time.perf_counter() - t0
+
+    # ---- cross-rank facts: per-rank times, world size, data-parallel parameter agreement
+    times = torch.zeros(world, dtype=torch.float64, device=dev)
+    times[rank] = mine
+    dist.all_reduce(times)
+    sec = float(times.max().item())
+    optimizer.wait_param_sync()
+    ck = _param_checksum(model, dev)
+    cks = [torch.zeros_like(ck) for _ in range(dp)]
+    dist.all_gather(cks, ck, group=topology.data_parallel_group)
+    dp_agree = bool(all(torch.equal(cks[0], c) for c in cks[1:]))
+    agree_t = torch.tensor([1.0 if dp_agree else 0.0], device=dev)
+    dist.all_reduce(agree_t, op=dist.ReduceOp.MIN)
+    dp_agree = bool(agree_t.item() == 1.0)
+    _, unique_params = model.get_params_count()
+
     gbs = config.topology.global_batch_size
     tokens = gbs * a.seq_len * a.steps
     ms = 1000.0 * sec / a.steps
     if rank == 0:
-        headline = a.num_layers is None and a.model == "llama2_7b" and a.seq_len == 4096
+        headline = (a.num_layers is None and a.model == "llama2_7b" and a.seq_len == 4096 and gpu
+                    and a.precision == "bfloat16")
+        flops_tok = 6 * unique_params + 12 * arch["num_layers"] * arch["hidden_size"] * a.seq_len
+        if a.lora:  # frozen base: no weight-gradient GEMMs for the base weights (~1/3 of the 6N)
+            flops_tok = None
+        parallelism = (f"tp{a.tp}_pp{a.pp}_dp{dp}" + ("_zero1" if a.zero else "") +
+                       (f"_ac-{a.activation_checkpointing}" if a.activation_checkpointing != "disabled" else "") +
+                       ("_sp" if a.sequence_parallel else "") + ("_lora" if a.lora else ""))
         res = {
-            "metric": "tokens/sec (whole node) Llama-2-7B-shape bf16, TP×PP×DP on 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": tokens / sec,
             "unit": "tokens/s",
             "n_gpus": world,
@@ -169,33 +307,41 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.precision == "bfloat16" else "fp32",
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
                 "model": ("Llama-2-7B-shape (h4096 L32 heads32 kv8 GQA, SwiGLU 11008, RoPE, RMSNorm, V32000)"
                           if headline else f"{a.model} layers={arch['num_layers']} seq={a.seq_len} (NOT headline)"),
                 "global_batch": gbs,
                 "seq_len": a.seq_len,
-                "parallelism": f"tp{a.tp}_pp{a.pp}_dp{dp}" + ("_zero1" if a.zero else "") +
-                               (f"_ac-{a.activation_checkpointing}" if a.activation_checkpointing != "disabled" else "") +
-                               ("_sp" if a.sequence_parallel else ""),
+                "parallelism": parallelism,
                 "micro_batch": a.micro_batch,
                 "grad_acc": a.grad_acc,
                 "loss": None if last is None else last.loss,
-                "mfu_palm": None,
+                "mfu_palm": None if flops_tok is None or not gpu else (tokens / sec) * flops_tok / (2.5166e15 * world),
                 "gemm_tuning": gemm_mode,
+                "params": unique_params,
+                "backend": dist.get_backend(),
+                "world_size_seen": dist.get_world_size(),
+                "per_rank_ms_per_step": [round(1000.0 * float(t) / a.steps, 2) for t in times.tolist()],
+                "dp_param_checksum_agree": dp_agree,
             },
         }
-        n_params = sum(p.numel() for p in model.parameters()) * a.tp * a.pp if a.pp == 1 else None
-        if n_params:
-            flops_tok = 6 * n_params + 12 * arch["num_layers"] * arch["hidden_size"] * a.seq_len
-            res["config"]["mfu_palm"] = (tokens / sec) * flops_tok / (2.5166e15 * world)
         if a.profile_json:
             with open(a.profile_json, "w") as f:
                 json.dump({"per_step_s": per_step, **res}, f)
         print(json.dumps(res), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    if not dp_agree:
+        raise SystemExit("data-parallel replicas diverged (parameter checksums differ)")
+
+
+def main() -> None:
+    a = _args()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(_launch(a))
+    _worker(a)
 
 
 if __name__ == "__main__":

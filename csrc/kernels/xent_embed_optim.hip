@@ -12,14 +12,14 @@ template <typename T>
 __global__ __launch_bounds__(256) void xent_stats_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                          int64_t rows, int V, int64_t v0, float* __restrict__ m_out,
                                                          float* __restrict__ s_out, float* __restrict__ t_out,
-                                                         int64_t* __restrict__ amax_out) {
+                                                         int64_t* __restrict__ amax_out, int vec) {
     __shared__ float sm[4], ss[4];
     __shared__ int si[4];
     const int64_t row = blockIdx.x;
     const T* x = logits + row * (int64_t)V;
     float m = -INFINITY, s = 0.f;
     int am = 0;
-    const int nv = V / 8;
+    const int nv = vec ? V / 8 : 0;  // 16-byte vector path only for aligned rows (V % 8 == 0, aligned base)
     for (int i = threadIdx.x; i < nv; i += 256) {
         float v[8];
         V8<T>::ld(x + i * 8, v);
@@ -75,13 +75,13 @@ __global__ __launch_bounds__(256) void xent_stats_kernel(const T* __restrict__ l
 template <typename T>
 __global__ __launch_bounds__(256) void xent_bwd_kernel(const T* logits, const int64_t* __restrict__ tgt,
                                                        const float* __restrict__ lse, const float* __restrict__ gscale,
-                                                       T* dlogits, int64_t rows, int V, int64_t v0) {
+                                                       T* dlogits, int64_t rows, int V, int64_t v0, int vec) {
     const int64_t row = blockIdx.x;
     const T* x = logits + row * (int64_t)V;
     T* d = dlogits + row * (int64_t)V;
     const float L = lse[row], g = gscale[row];
     const int64_t t = tgt[row] - v0;
-    const int nv = V / 8;
+    const int nv = vec ? V / 8 : 0;
     for (int i = threadIdx.x; i < nv; i += 256) {
         float v[8];
         V8<T>::ld(x + i * 8, v);
@@ -148,10 +148,10 @@ template <typename G, typename P>
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, P* __restrict__ pout,
                                                     int64_t n, float lr, float b1, float b2, float eps, float wd,
-                                                    float bc1, float bc2_sqrt, float gscale) {
+                                                    float bc1, float bc2_sqrt, float gscale, int vec) {
     const float step = lr / bc1;
     const float decay = 1.f - lr * wd;
-    const int64_t n4 = n / 4;
+    const int64_t n4 = vec ? n / 4 : 0;  // f32x4 path only when p/m/v are 16-byte aligned
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
         f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
         f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
@@ -253,19 +253,24 @@ static int gridn(int64_t n, int per = 256, int cap = 4096) {
 }
 
 namespace sa_launch {
+static inline int xent_vec_ok(const void* a, const void* b, int V) {
+    return (V % 8 == 0) && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) % 16 == 0);
+}
 void xent_stats(int dtype, const void* logits, const int64_t* tgt, int64_t rows, int V, int64_t v0, float* m, float* s,
                 float* t, int64_t* amax, hipStream_t st) {
     if (rows == 0) return;
-    if (dtype == DT_BF16) hipLaunchKernelGGL(xent_stats_kernel<u16>, dim3(rows), 256, 0, st, (const u16*)logits, tgt, rows, V, v0, m, s, t, amax);
-    else if (dtype == DT_F16) hipLaunchKernelGGL(xent_stats_kernel<f16>, dim3(rows), 256, 0, st, (const f16*)logits, tgt, rows, V, v0, m, s, t, amax);
-    else hipLaunchKernelGGL(xent_stats_kernel<float>, dim3(rows), 256, 0, st, (const float*)logits, tgt, rows, V, v0, m, s, t, amax);
+    const int vec = xent_vec_ok(logits, logits, V);
+    if (dtype == DT_BF16) hipLaunchKernelGGL(xent_stats_kernel<u16>, dim3(rows), 256, 0, st, (const u16*)logits, tgt, rows, V, v0, m, s, t, amax, vec);
+    else if (dtype == DT_F16) hipLaunchKernelGGL(xent_stats_kernel<f16>, dim3(rows), 256, 0, st, (const f16*)logits, tgt, rows, V, v0, m, s, t, amax, vec);
+    else hipLaunchKernelGGL(xent_stats_kernel<float>, dim3(rows), 256, 0, st, (const float*)logits, tgt, rows, V, v0, m, s, t, amax, vec);
 }
 void xent_bwd(int dtype, const void* logits, const int64_t* tgt, const float* lse, const float* gscale, void* dlogits,
               int64_t rows, int V, int64_t v0, hipStream_t st) {
     if (rows == 0) return;
-    if (dtype == DT_BF16) hipLaunchKernelGGL(xent_bwd_kernel<u16>, dim3(rows), 256, 0, st, (const u16*)logits, tgt, lse, gscale, (u16*)dlogits, rows, V, v0);
-    else if (dtype == DT_F16) hipLaunchKernelGGL(xent_bwd_kernel<f16>, dim3(rows), 256, 0, st, (const f16*)logits, tgt, lse, gscale, (f16*)dlogits, rows, V, v0);
-    else hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), 256, 0, st, (const float*)logits, tgt, lse, gscale, (float*)dlogits, rows, V, v0);
+    const int vec = xent_vec_ok(logits, dlogits, V);
+    if (dtype == DT_BF16) hipLaunchKernelGGL(xent_bwd_kernel<u16>, dim3(rows), 256, 0, st, (const u16*)logits, tgt, lse, gscale, (u16*)dlogits, rows, V, v0, vec);
+    else if (dtype == DT_F16) hipLaunchKernelGGL(xent_bwd_kernel<f16>, dim3(rows), 256, 0, st, (const f16*)logits, tgt, lse, gscale, (f16*)dlogits, rows, V, v0, vec);
+    else hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), 256, 0, st, (const float*)logits, tgt, lse, gscale, (float*)dlogits, rows, V, v0, vec);
 }
 void embed_fwd(int dtype, const int64_t* ids, const void* W, void* out, int64_t ntok, int H, int64_t v0, int64_t Vp,
                hipStream_t st) {
@@ -286,8 +291,9 @@ void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* s
 void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, void* pout, int64_t n, float lr,
            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale, hipStream_t st) {
     if (n == 0) return;
-    const int grid = gridn(n / 4 + 1, 256, 8192);
-#define SA_ADAM(GT, PT) hipLaunchKernelGGL((adamw_kernel<GT, PT>), grid, 256, 0, st, p, (const GT*)g, m, v, (PT*)pout, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale)
+    const int vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) % 16) == 0;
+    const int grid = gridn(vec ? n / 4 + 1 : n, 256, 8192);
+#define SA_ADAM(GT, PT) hipLaunchKernelGGL((adamw_kernel<GT, PT>), grid, 256, 0, st, p, (const GT*)g, m, v, (PT*)pout, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, vec)
     if (gdtype == DT_F32) {
         if (pdtype == DT_BF16) SA_ADAM(float, u16); else if (pdtype == DT_F16) SA_ADAM(float, f16); else SA_ADAM(float, float);
     } else if (gdtype == DT_BF16) {

@@ -16,6 +16,7 @@ import torch.distributed as dist
 
 from ..config import BaseConfig
 from ..topology import Topology, TopologyState
+from ..utils.safe_load import safe_load
 
 
 class ContextState(TypedDict):
@@ -100,8 +101,7 @@ class BaseContext:
         dir = Path(dir)
         f = dir / f"context_global_rank_{self.topology.config.global_rank}.pt"
         if f.is_file():
-            # our own file: contains python/numpy RNG tuples, so it needs the full unpickler
-            self.load_state_dict(torch.load(str(f), weights_only=False))
+            self.load_state_dict(safe_load(f))
         if self.topology.is_distributed_initialized:
             vals = [self.iterations, self.consumed_samples, self.consumed_samples_evaluation]
             if self.topology.config.global_rank != 0:

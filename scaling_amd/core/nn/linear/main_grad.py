@@ -9,6 +9,11 @@ temporary, no elementwise accumulate pass, and a single bf16 rounding of ``grad 
 The optimizer's bucket-ready callback (``_sa_grad_ready``) is invoked in place of autograd's
 post-accumulate-grad hook.
 
+A weight may carry ``_sa_grad_row_mask`` (``[N, 1]``, 0/1): rows whose mask is 0 receive no gradient
+(LM-head ``finetunable_token_ids``; reference ``transformer/model/layers/lm_head.py:34-53`` masks with a
+tensor hook, which a GEMM-accumulated gradient would bypass).  The mask is folded into the output
+gradient's columns before the weight-gradient GEMM, so both gradient paths honour it.
+
 Several weights that read the same input (q/k/v, SwiGLU ``dense_in``/``siglu_weight``) run as ONE
 GEMM.  When the weights (and their gradients) sit back to back in the flat buffers the combined
 ``[sum N, K]`` matrix is a zero-copy strided view; otherwise it is concatenated.
@@ -77,6 +82,11 @@ class _MultiLinear(torch.autograd.Function):
         if any(ctx.needs_input_grad[2 : 2 + n]):
             g2 = g.reshape(-1, g.shape[-1])
             x2 = x.reshape(-1, x.shape[-1])
+            masks = [getattr(wt, "_sa_grad_row_mask", None) for wt in weights]
+            if any(m is not None for m in masks):
+                col = torch.cat([m.reshape(-1).to(g2.device, g2.dtype) if m is not None else g2.new_ones(s)
+                                 for m, s in zip(masks, ctx.splits)])
+                g2 = g2 * col
             target = _main_grad_target(weights)
             if target is not None:
                 wgrad(g2, x2, target, accumulate=True)

@@ -86,21 +86,40 @@ def _to_python(x: Any) -> Any:
 
 
 class _StepTimer:
-    def __init__(self) -> None:
+    """Step duration from HIP events on the compute stream (no device-wide synchronize).
+
+    A device-wide sync at the step boundary would also wait for the ZeRO parameter all-gathers the
+    optimizer leaves in flight on its comm stream, which are meant to overlap the next forward.
+    The end event is waited on alone; the step's loss read-back has already drained the compute
+    stream, so this costs nothing extra."""
+
+    def __init__(self, device: Optional[torch.device] = None) -> None:
+        self.device = device
         self.t0 = 0.0
         self.t1 = 0.0
+        self._ev0: Optional[Any] = None
+        self._ev1: Optional[Any] = None
+
+    def _gpu(self) -> bool:
+        return self.device is not None and self.device.type == "cuda"
 
     def start(self) -> None:
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
         self.t0 = time.perf_counter()
+        if self._gpu():
+            self._ev0 = torch.cuda.Event(enable_timing=True)
+            self._ev0.record(torch.cuda.current_stream(self.device))
 
     def stop(self) -> None:
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
+        if self._gpu():
+            self._ev1 = torch.cuda.Event(enable_timing=True)
+            self._ev1.record(torch.cuda.current_stream(self.device))
+            self._ev1.synchronize()
         self.t1 = time.perf_counter()
 
     def duration(self) -> float:
+        if self._ev0 is not None and self._ev1 is not None:
+            # wall time covers the host-side start latency before the first kernel too
+            return max(self.t1 - self.t0, self._ev0.elapsed_time(self._ev1) / 1000.0)
         return self.t1 - self.t0
 
 
@@ -124,12 +143,15 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         self.communicator_loss_out: Optional[PipeCommunicator] = None
         if topology.config.pipe_parallel_size > 1:
             if topology.is_first_pipe_parallel_rank:
-                self.communicator_loss_in = PipeCommunicator(dev, recv_grads=False, recv_data=True)
+                # loss + metrics may hold python values that change every step: continuous mode
+                self.communicator_loss_in = PipeCommunicator(dev, recv_grads=False, recv_data=True,
+                                                             use_continuous_recommunication=True)
             if topology.is_last_pipe_parallel_rank:
-                self.communicator_loss_out = PipeCommunicator(dev, recv_grads=False, recv_data=False)
+                self.communicator_loss_out = PipeCommunicator(dev, recv_grads=False, recv_data=False,
+                                                              use_continuous_recommunication=True)
         self.profiler = Profiler(config=profiler_config, topology=topology)
         self._param_sync_optimizer: Optional[BaseOptimizer] = None
-        self.step_timer = _StepTimer()
+        self.step_timer = _StepTimer(dev)
         self.broadcast_model()
 
     # ------------------------------------------------------------------ parameters
@@ -269,6 +291,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                 else:
                     raise NotImplementedError(f"Instruction '{ins.__class__.__name__}' not implemented")
         loss, metrics = self.get_loss(metrics_aggregation_fn)
+        self.wait_pending_sends()
         self.profiler.flush()
         self.step_timer.stop()
         assert opt_out is not None
@@ -300,6 +323,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                 else:
                     raise NotImplementedError(f"Instruction '{ins.__class__.__name__}' not implemented")
         loss, metrics = self.get_loss(metrics_aggregation_fn)
+        self.wait_pending_sends()
         self.profiler.flush()
         self.step_timer.stop()
         self._layers.train()
@@ -321,6 +345,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                 self._execute_receive_activations(ins.buffer_id)
             else:
                 raise NotImplementedError(f"Instruction '{ins.__class__.__name__}' not implemented for run_instructions.")
+        self.wait_pending_sends()
         topo = self.topology
         if batch is not None and topo.config.pipe_parallel_size == 1 and ins is not None:
             out = self.pipe_buffer.take(BufferType.PIPELINE_STAGE_OUTPUT, ins.buffer_id)
@@ -405,6 +430,15 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                 for p in layer.parameters():
                     if p.core_parameter_meta.tied_grad_on_model_parallel and p.grad is not None:
                         allreduce_tensor_in_float32(p.grad, process_group=self.topology.model_parallel_group)
+
+    def _communicators(self) -> list[PipeCommunicator]:
+        return [c for c in (self.communicator_in, self.communicator_out, self.communicator_loss_in,
+                            self.communicator_loss_out) if c is not None]
+
+    def wait_pending_sends(self) -> None:
+        """Retires the asynchronous pipeline sends of this step (their buffers may be freed after)."""
+        for c in self._communicators():
+            c.wait_pending_sends()
 
     def reset_activation_shape(self) -> None:
         self.communicator_in.reset_communication_meta()

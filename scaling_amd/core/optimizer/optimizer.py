@@ -34,6 +34,7 @@ from ...ops import optim as optim_ops
 from ..logging import logger
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
+from ..utils.safe_load import safe_load
 from .base import BaseOptimizer, OptimizerStepOutput
 from .loss_scaler import LossScaler
 from .optimizer_config import OptimizerConfig
@@ -130,11 +131,7 @@ class Optimizer(BaseOptimizer):
                 else:
                     scratch = self._scratch[: g.bucket_size]
                     optim_ops.cast_scale_(src, scratch, inv)
-                    if self._gpu:
-                        dist.reduce_scatter_tensor(out, scratch, group=group)
-                    else:  # gloo: reduce-scatter via all-reduce
-                        dist.all_reduce(scratch, group=group)
-                        out.copy_(scratch[g.dp_rank * g.chunk : (g.dp_rank + 1) * g.chunk])
+                    dist.reduce_scatter_tensor(out, scratch, group=group)
             else:
                 optim_ops.cast_scale_(src, out, inv)
                 dist.all_reduce(out, group=group)
@@ -245,11 +242,8 @@ class Optimizer(BaseOptimizer):
                 ev = torch.cuda.Event()
                 ev.record(self._comm_stream)
             self._ag_events[(gi, b)] = ev
-        elif self._gpu:
-            dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
         else:
-            parts = list(full.view(self.dp, g.chunk).unbind(0))
-            dist.all_gather(parts, mine.clone(), group=self.topology.data_parallel_group)
+            dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
 
     def step(self) -> OptimizerStepOutput:
         self.wait_param_sync()  # parameters never touched by a forward (frozen / unused) still must land
@@ -357,11 +351,7 @@ class Optimizer(BaseOptimizer):
         if not self.config.zero or self.dp == 1:
             return mine
         full = torch.empty(g.bucket_size, dtype=buf.dtype, device=buf.device)
-        if self._gpu:
-            dist.all_gather_into_tensor(full, mine.contiguous(), group=self.topology.data_parallel_group)
-        else:
-            parts = list(full.view(self.dp, g.chunk).unbind(0))
-            dist.all_gather(parts, mine.contiguous(), group=self.topology.data_parallel_group)
+        dist.all_gather_into_tensor(full, mine.contiguous(), group=self.topology.data_parallel_group)
         return full
 
     def _full_param_states(self) -> dict[int, list[tuple[torch.Tensor, dict[str, torch.Tensor]]]]:
@@ -430,7 +420,7 @@ class Optimizer(BaseOptimizer):
         topo = self.topology
         if self.config.zero and self.config.zero_save_static:
             f = directory / f"optimizer_state_static_mp_{topo.model_parallel_rank}_pp_{topo.pipe_parallel_rank}_dp_{topo.data_parallel_rank}.pt"
-            sd = torch.load(str(f), map_location=topo.device, weights_only=False)  # own file format
+            sd = safe_load(f, map_location=topo.device)
             self.step_index = sd["step_index"]
             self.loss_scaler.load_state_dict(sd["loss_scaler"])
             for g, s in zip(self.parameter_groups, sd["parameter_groups"]):
@@ -451,7 +441,7 @@ class Optimizer(BaseOptimizer):
             f = directory / f"optimizer_state_layer_{li}.pt"
             if not f.is_file():
                 continue
-            d = torch.load(str(f), map_location="cpu", weights_only=False)  # own file format (contains sets)
+            d = safe_load(f, map_location="cpu")
             first = first or d
             for _, ps in d["parameters"].items():
                 meta = CoreParameterMeta.from_state_dict(ps["meta"])

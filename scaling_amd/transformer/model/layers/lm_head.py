@@ -47,7 +47,8 @@ class TransformerLMHead(TransformerLayerBaseIO):
                 if rank * self.vocab_per_rank <= t < (rank + 1) * self.vocab_per_rank:
                     mask[t - rank * self.vocab_per_rank] = 1
             self.register_buffer("_finetune_mask", mask, persistent=False)
-            self.linear.weight.register_hook(lambda g: None if g is None else g * self._finetune_mask)
+            # honoured by the GEMM-fused weight-gradient path (core/nn/linear/main_grad.py)
+            self.linear.weight._sa_grad_row_mask = self._finetune_mask  # type: ignore[attr-defined]
 
     def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
         return _finish(self, x, self.linear(x.activations), self.vocab_per_rank)

@@ -1,0 +1,65 @@
+"""bench.py contract on CPU (gloo plumbing mode): self-launch of N ranks, one JSON line, fail-fast."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args: list[str], env_extra: dict | None = None, timeout: int = 600) -> subprocess.CompletedProcess:
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_lines(out: str) -> list[dict]:
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+TINY = ["--model", "llama_tiny", "--backend", "gloo", "--seq-len", "64", "--micro-batch", "1", "--steps", "2",
+        "--warmup", "1"]
+
+
+@pytest.mark.parametrize("layout", [("4", "2", "2", "2"), ("8", "2", "2", "4"), ("2", "1", "1", "2")])
+def test_bench_self_launch_gloo(layout):
+    gpus, tp, pp, acc = layout
+    r = _run(["--gpus", gpus, "--tp", tp, "--pp", pp, "--grad-acc", acc, *TINY])
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    res = lines[0]
+    n = int(gpus)
+    dp = n // (int(tp) * int(pp))
+    assert res["n_gpus"] == n and res["config"]["world_size_seen"] == n
+    assert res["config"]["parallelism"].startswith(f"tp{tp}_pp{pp}_dp{dp}")
+    assert res["config"]["global_batch"] == dp * int(acc)
+    assert len(res["config"]["per_rank_ms_per_step"]) == n
+    assert res["config"]["dp_param_checksum_agree"] is True
+    assert res["value"] > 0 and res["steps"] == 2 and res["warmup"] == 1
+    assert res["value"] == pytest.approx(res["config"]["global_batch"] * 64 * 2 / (res["ms_per_step"] * 2 / 1000.0))
+    assert "NOT headline" in res["config"]["model"]
+
+
+def test_bench_lora_gloo():
+    r = _run(["--gpus", "2", "--lora", "--lora-rank", "8", "--grad-acc", "2", *TINY])
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _json_lines(r.stdout)[0]
+    assert res["config"]["parallelism"].endswith("_lora") and res["config"]["dp_param_checksum_agree"]
+
+
+def test_bench_launcher_fail_fast():
+    t0 = time.time()
+    r = _run(["--gpus", "4", "--tp", "2", *TINY], env_extra={"BENCH_FAIL_RANK": "1"}, timeout=300)
+    assert r.returncode != 0
+    assert "rank 1 exited with 3" in r.stderr
+    assert _json_lines(r.stdout) == []
+    assert time.time() - t0 < 120

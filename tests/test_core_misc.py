@@ -132,36 +132,6 @@ def test_schedule_visualize(tmp_path):
     assert (tmp_path / "train.png").stat().st_size > 0
 
 
-# ---------------------------------------------------------------- pipe communicator (2 ranks)
-def _pipe_comm_case():
-    import torch.distributed as dist
-
-    from scaling_amd.core.nn.parallel_module.communicator import PipeCommunicator
-
-    make_topology(pipe_parallel_size=2)
-    rank = dist.get_rank()
-    comm = PipeCommunicator(torch.device("cpu"), recv_grads=True, recv_data=True)
-    for step in range(3):  # meta sent once, later only payloads
-        if rank == 0:
-            x = torch.full((2, 3), float(step), requires_grad=True)
-            comm.send_data((x, torch.arange(4), ["names", step]), 1)
-            g = comm.recv_gradients((x,), 1)
-            assert torch.equal(g.grad_tensors[0], torch.full((2, 3), 2.0 * step))
-        else:
-            t = comm.recv_data(0)
-            assert torch.equal(t[0], torch.full((2, 3), float(step))) and torch.equal(t[1], torch.arange(4))
-            assert t[2] == ["names", step]
-            comm.send_gradients((t[0],), 0) if False else None
-            y = t[0]
-            y.grad = 2 * y.detach()
-            comm.send_gradients((y,), 0)
-    return True
-
-
-def test_pipe_communicator_roundtrip():
-    assert all(run_distributed(_pipe_comm_case, 2).values())
-
-
 # ---------------------------------------------------------------- runner
 def test_runner_host_parsing_and_payload():
     from scaling_amd.core.runner.launch_config import decode_base64

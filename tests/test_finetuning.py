@@ -162,8 +162,12 @@ def test_finetuning_with_ignore_keys_in_checkpoint(tmp_path, mp, pp, world):
 @needs_fixtures
 @pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (1, 2, 2)])
 @pytest.mark.parametrize("finetunable", [["embedding.weight"], ["embedding.weight", "mlp.dense_in.weight"]])
-def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
-    """Only the rows of ``finetunable_token_ids`` of the (tied) embedding may change."""
+@pytest.mark.parametrize("tied", [True, False])
+def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable, tied):
+    """Only the rows of ``finetunable_token_ids`` of the embedding (and of the untied LM head, whose
+    weight gradient is accumulated by the GEMM) may change."""
+    if not tied:
+        finetunable = finetunable + ["linear.weight"]
     sys.path.insert(0, str(ROOT))
     from scaling_amd.core import MemoryMapDatasetBuilder
     from scaling_amd.transformer.tokenizer import Tokenizer
@@ -178,7 +182,7 @@ def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
             b.add(np.array(ids))
     cfg = _config(tmp_path, mp, pp, world, mbs=1, memory_map=True, data_prefixes=[prefix])
     cfg["training"]["finetune"] = True
-    cfg["transformer_architecture"]["weight_tying"] = True
+    cfg["transformer_architecture"]["weight_tying"] = tied
     cfg["transformer_architecture"]["finetunable_token_ids"] = rows
     cfg["training"]["finetunable_parameters"] = finetunable
     _run(tmp_path, cfg, world, "pre")
@@ -187,6 +191,7 @@ def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
     _run(tmp_path, cfg, world, "ft")
     ck = tmp_path / "ckpt"
     reached = [False, False]
+    head_checked = tied
     for f in (ck / "global_step6").glob("model_state*.pt"):
         if "EmbeddingInput" not in f.name and "LMHead" not in f.name:
             continue
@@ -194,6 +199,8 @@ def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
         for name in finetunable:
             if name not in s2:
                 continue
+            if name == "linear.weight" and "LMHead" in f.name:
+                head_checked = True
             for tid, (a, b) in enumerate(zip(s2[name], s4[name])):
                 if tid in rows:
                     reached[0] = True
@@ -201,4 +208,4 @@ def test_finetune_embedding_rows(tmp_path, mp, pp, world, finetunable):
                 else:
                     reached[1] = True
                     assert torch.equal(a, b), f"row {tid} changed"
-    assert all(reached)
+    assert all(reached) and head_checked

@@ -231,11 +231,15 @@ def test_rope_flash_attention_fused(qkv_in_one):
     torch.testing.assert_close(gf.float(), base.grad.float(), atol=1e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("V", [1000, 32000])
-def test_cross_entropy(V):
+@pytest.mark.parametrize("V,offset", [(1000, 0), (32000, 0), (50257, 0), (1001, 0), (32000, 3)])
+def test_cross_entropy(V, offset):
+    """Odd vocab sizes (rows not 16-B aligned) and a misaligned base take the scalar row path."""
     torch.manual_seed(0)
     N = 67
-    logits = (3 * torch.randn(N, V, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    base = torch.empty(N * V + offset, device=DEV, dtype=torch.bfloat16)
+    logits = base[offset:].view(N, V)
+    logits.copy_(3 * torch.randn(N, V, device=DEV))
+    logits = logits.detach().requires_grad_(True)
     tgt = torch.randint(0, V, (N,), device=DEV)
     loss, am = xent.vocab_parallel_cross_entropy(logits, tgt)
     lr = logits.detach().float().requires_grad_(True)
@@ -282,11 +286,29 @@ def test_adamw_matches_torch():
         g = torch.randn(n, device=DEV)
         ref.grad = g.clone()
         opt.step()
-        optim.adamw_step_(p, g.to(torch.bfloat16).float(), m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8,
-                          weight_decay=0.1, step=step, param_out=pout) if False else optim.adamw_step_(
-            p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step, param_out=pout)
+        optim.adamw_step_(p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step,
+                          param_out=pout)
     torch.testing.assert_close(p, ref.detach(), atol=1e-6, rtol=1e-5)
     torch.testing.assert_close(pout.float(), ref.detach(), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("offset", [1, 2, 3])
+def test_adamw_unaligned_views(offset):
+    """Buckets at element offsets that are not 16-B aligned (e.g. dp=3 chunks) use the scalar path."""
+    torch.manual_seed(0)
+    n = 4099
+    bufs = [torch.randn(n + offset, device=DEV) for _ in range(3)]
+    p, m, v = (b[offset:] for b in bufs)
+    m.zero_()
+    v.zero_()
+    ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV)
+        ref.grad = g.clone()
+        opt.step()
+        optim.adamw_step_(p, g, m, v, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=step)
+    torch.testing.assert_close(p, ref.detach(), atol=1e-6, rtol=1e-5)
 
 
 def test_sumsq():
