@@ -65,6 +65,7 @@ class Optimizer(BaseOptimizer):
         )
         self._launched: list[set[int]] = [set() for _ in parameter_groups]
         self._pending: list[list[int]] = [list(g.bucket_param_count) for g in parameter_groups]
+        self._reported: list[set[int]] = [set() for _ in parameter_groups]
         self._armed = False
         self._deferred = self._deferred_buckets()
         self._ag_events: dict[tuple[int, int], Any] = {}
@@ -101,9 +102,18 @@ class Optimizer(BaseOptimizer):
         return out
 
     def _make_hook(self, gi: int, pi: int):
+        """Gradient-final notification of parameter `pi`, counted once per armed backward.
+
+        A parameter reports either through the GEMM-fused weight-gradient path (``_sa_grad_ready``,
+        called right after the GEMM accumulated into ``.grad``) or through autograd's post-accumulate
+        hook.  PyTorch also fires that hook when the backward returned no gradient for the weight —
+        exactly the GEMM-fused case — so without de-duplication every such weight would count twice and
+        its bucket would be reduced before the rest of its gradients were written."""
+
         def hook(_p: torch.Tensor) -> None:
-            if not self._armed:
+            if not self._armed or pi in self._reported[gi]:
                 return
+            self._reported[gi].add(pi)
             for b in self.parameter_groups[gi].param_buckets[pi]:
                 self._pending[gi][b] -= 1
                 if self._pending[gi][b] == 0 and b not in self._deferred[gi]:
@@ -149,6 +159,7 @@ class Optimizer(BaseOptimizer):
             self._armed = True
             self._pending = [list(g.bucket_param_count) for g in self.parameter_groups]
             self._launched = [set() for _ in self.parameter_groups]
+            self._reported = [set() for _ in self.parameter_groups]
 
     def finish_grad_sync(self) -> None:
         if self.dp == 1:
