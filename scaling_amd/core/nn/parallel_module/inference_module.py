@@ -46,9 +46,11 @@ class HiddenStateRecorder:
 
     def start_recording(self) -> None:
         for li, s in self.recorder_settings_per_layer.items():
+            if s.include_modules is None and s.exclude_modules is None:
+                continue  # neither list given: nothing is recorded for this layer (reference semantics)
             layer = self._module._layers[li]
             for name, sub in layer.named_modules():
-                take = (name in s.include_modules) if s.include_modules is not None else (name not in (s.exclude_modules or ()))
+                take = (name in s.include_modules) if s.include_modules is not None else (name not in s.exclude_modules)
                 if take:
                     self._hooks.append(sub.register_forward_hook(partial(self.record_output, layer_index=li, name=name)))
 

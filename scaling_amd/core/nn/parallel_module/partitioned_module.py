@@ -52,7 +52,8 @@ class PipePartitionedModule(torch.nn.Module):
         self.devices: Optional[list[torch.device]] = None
         if devices is not None:
             self.devices = [
-                d if isinstance(d, torch.device) else (torch.device("cuda", d) if torch.cuda.is_available() else torch.device("cpu"))
+                d if isinstance(d, torch.device) else torch.device(d) if isinstance(d, str)
+                else (torch.device("cuda", d) if torch.cuda.is_available() else torch.device("cpu"))
                 for d in devices
             ]
         self._layer_specs = layer_specs
