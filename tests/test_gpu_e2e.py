@@ -152,9 +152,7 @@ def test_gpu_cached_generation_matches_uncached(kernel):
     prompt = [3, 17, 42, 99, 5, 7, 11]
     a = m.generate(12, input_tokens=prompt, stop_tokens=[], use_cache=True)
     b = m.generate(12, input_tokens=prompt, stop_tokens=[], use_cache=False)
-    n = 0
-    while n < min(len(a.completion_tokens), len(b.completion_tokens)) and a.completion_tokens[n] == b.completion_tokens[n]:
-        n += 1
-    assert n >= 1, (a.completion_tokens, b.completion_tokens)
-    la, lb = a.completion_logits[:n].float().cpu(), b.completion_logits[:n].float().cpu()
+    assert len(a.completion_tokens) == len(b.completion_tokens) == 12
+    assert a.completion_tokens == b.completion_tokens, (a.completion_tokens, b.completion_tokens)
+    la, lb = a.completion_logits.float().cpu(), b.completion_logits.float().cpu()
     torch.testing.assert_close(la, lb, rtol=5e-2, atol=5e-2)
