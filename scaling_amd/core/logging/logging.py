@@ -143,9 +143,13 @@ class _LoggerSingleton:
         self._instance = Logger(config=config, name=name, global_rank=global_rank)
 
     def configure_determined(
-        self, config: LoggerConfig, name: Optional[str] = None, global_rank: Optional[int] = None, **_: Any
+        self, config: LoggerConfig, name: Optional[str] = None, global_rank: Optional[int] = None,
+        determined_context: Any = None, **_: Any
     ) -> None:
+        """Like ``configure``; metrics of the ranks in ``determined_metrics_ranks`` also go to the trial."""
         self.configure(config, name=name, global_rank=global_rank)
+        assert self._instance is not None
+        self._instance.configure_determined(determined_context)
 
     def __getattr__(self, item: str) -> Any:
         if self._instance is None:

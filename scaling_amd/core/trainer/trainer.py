@@ -222,33 +222,137 @@ class DeterminedBaseTrainer(BaseTrainer[DeterminedBaseContextGeneric, ParallelMo
     """Trainer with Determined-cluster checkpoint storage and preemption (optional dependency).
 
     Without a Determined context (``context._use_determined`` False) it behaves exactly like
-    ``BaseTrainer``.  With one it resumes from ``info.latest_checkpoint``, reports checkpoints and
-    exits cleanly on preemption (reference ``trainer.py:317-558``).
+    ``BaseTrainer``.  With one (reference ``trainer.py:317-558``) it
+    * resumes from the trial's ``latest_checkpoint`` (pause/resume of an experiment), forcing optimizer
+      and context state to load;
+    * stores checkpoints through ``checkpoint.store_path`` and, with ``delete_past_optimizer_states``,
+      removes the optimizer-state files of every older completed checkpoint of the trial;
+    * on construction (rank 0) deletes checkpoints written off the ``save_interval`` grid (preemption
+      saves), keeping the newest one for resuming;
+    * saves and exits when the cluster asks for preemption, and advances the profiler agent per step.
+
+    The cluster is reached only through ``_cluster_info`` and ``_trial_checkpoints`` (objects with the
+    Determined API's ``uuid``/``metadata``/``state``/``delete``/``remove_files``), so the logic runs and
+    is tested against duck-typed stand-ins where ``determined`` is not installed.
     """
 
+    def __init__(self, *args: Any, **kwargs: Any) -> None:
+        super().__init__(*args, **kwargs)
+        if self.context.topology.config.global_rank == 0 and self._use_determined():
+            self.delete_preempted_checkpoints_determined()
+
+    # ------------------------------------------------------------------ cluster access (overridable)
+    def _use_determined(self) -> bool:
+        return bool(getattr(self.context, "_use_determined", False)) and getattr(self.context, "determined_context", None) is not None
+
+    def _cluster_info(self) -> Any:
+        try:
+            import determined as det  # type: ignore
+        except ImportError:
+            return None
+        return det.get_cluster_info()
+
+    def _trial_checkpoints(self) -> list[Any]:
+        """Checkpoints of this trial, oldest (lowest batch number) first."""
+        import determined as det  # type: ignore
+        from determined.experimental import client  # type: ignore
+
+        info = self._cluster_info()
+        assert info is not None
+        trial = client.get_trial(info.trial.trial_id)
+        return list(trial.get_checkpoints(sort_by=det.experimental.client.CheckpointSortBy.BATCH_NUMBER,
+                                          order_by=det.experimental.client.CheckpointOrderBy.ASC))
+
+    @staticmethod
+    def _completed(ckpt: Any) -> bool:
+        st = getattr(ckpt, "state", None)
+        return str(getattr(st, "name", st)).upper().endswith("COMPLETED")
+
+    # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, save_dir: Optional[Path] = None) -> Path:
-        ctx = getattr(self.context, "determined_context", None)
-        if not getattr(self.context, "_use_determined", False) or ctx is None:
+        if not self._use_determined():
             return super().save_checkpoint(save_dir)
-        path = None
+        ctx = self.context.determined_context
         if self.context.topology.config.global_rank == 0:
             metadata = {"steps_completed": self.context.iterations}
-            with ctx.checkpoint.store_path(metadata) as (p, _storage_id):
+            with ctx.checkpoint.store_path(metadata) as (p, storage_id):
                 ctx.distributed.broadcast(str(p))
                 path = Path(p)
                 super().save_checkpoint(save_dir=path)
+            if self.config.delete_past_optimizer_states:
+                self.delete_previous_optimizer_states_determined(str(storage_id))
         else:
             path = Path(ctx.distributed.broadcast(None))
             super().save_checkpoint(save_dir=path)
         return path
 
+    def load_checkpoint(self, load_dir: Optional[Path] = None, load_optimizer_states: bool = True,
+                        load_context: bool = True, allowed_missing_keys_in_checkpoint: Optional[list[str]] = None,
+                        allowed_unexpected_keys_in_checkpoint: Optional[list[str]] = None,
+                        ignore_keys_in_checkpoint: Optional[list[str]] = None) -> bool:
+        kw = dict(allowed_missing_keys_in_checkpoint=allowed_missing_keys_in_checkpoint,
+                  allowed_unexpected_keys_in_checkpoint=allowed_unexpected_keys_in_checkpoint,
+                  ignore_keys_in_checkpoint=ignore_keys_in_checkpoint)
+        info = self._cluster_info() if self._use_determined() else None
+        latest = getattr(info, "latest_checkpoint", None) if info is not None else None
+        if latest is not None:
+            # a paused / preempted trial continues exactly where it stopped
+            with self.context.determined_context.checkpoint.restore_path(latest) as path:
+                logger.info(f"Updating load checkpoint directory from {load_dir} to {path} according to determined")
+                return super().load_checkpoint(load_dir=Path(path), load_optimizer_states=True, load_context=True, **kw)
+        return super().load_checkpoint(load_dir=load_dir, load_optimizer_states=load_optimizer_states,
+                                       load_context=load_context, **kw)
+
+    def delete_preempted_checkpoints_determined(self) -> list[str]:
+        """Deletes checkpoints saved off the ``save_interval`` grid except the newest; returns their uuids."""
+        if os.environ.get("DETERMINED_TEST") == "True":
+            return []
+        deleted: list[str] = []
+        try:
+            ckpts = self._trial_checkpoints()
+            for c in ckpts[:-1]:  # the newest stays: a paused trial resumes from it
+                steps = int(c.metadata["steps_completed"])
+                if self.config.save_interval and steps % self.config.save_interval != 0:
+                    logger.warning(f"Delete determined checkpoint {c.uuid} at step {steps} - likely saved at preemption")
+                    c.delete()
+                    deleted.append(str(c.uuid))
+        except Exception as ex:  # noqa: BLE001 - cluster API failures must not stop training
+            logger.error(f"deletion of previous determined preempted checkpoints failed, will not delete anything: {ex}")
+        return deleted
+
+    def delete_previous_optimizer_states_determined(self, latest_uuid: str) -> list[str]:
+        """Removes ``optimizer_state*`` files from every completed checkpoint but ``latest_uuid`` (rank 0)."""
+        if os.environ.get("DETERMINED_TEST") == "True" or self.context.topology.config.global_rank != 0:
+            return []
+        cleaned: list[str] = []
+        try:
+            for c in self._trial_checkpoints():
+                if str(c.uuid) != latest_uuid and self._completed(c):
+                    logger.info(f"Requesting optimizer states deletion of ckpt {c.uuid}")
+                    c.remove_files(["global_step*/*optimizer_state*pt"])
+                    cleaned.append(str(c.uuid))
+        except Exception as ex:  # noqa: BLE001
+            logger.error(f"deletion of previous optimizer states failed, will not delete anything: {ex}")
+            logger.error(f"DET_ENV_VARS_AFTER_FAILURE: { {k: v for k, v in os.environ.items() if k.startswith('DET_')} }")
+        return cleaned
+
+    # ------------------------------------------------------------------ loop
     def run_training(self, return_metrics: bool = False) -> Optional[list[dict[str, Any]]]:
-        ctx = getattr(self.context, "determined_context", None)
-        if ctx is None:
+        if not self._use_determined():
             return super().run_training(return_metrics)
+        ctx = self.context.determined_context
+        profiler = getattr(self.context, "determined_profiler", None)
         out: list[dict[str, Any]] = []
         while self.context.iterations < (self.config.train_iterations or 0):
+            if profiler is not None:
+                profiler.update_batch_idx(self.context.iterations)
             tso = self.train_step()
+            if ctx.preempt.should_preempt():
+                self.save_checkpoint()
+                print("exiting program after preemption.", flush=True)
+                if os.environ.get("DETERMINED_TEST") != "True":
+                    raise SystemExit(0)
+                break
             if self.config.save_interval is not None and self.context.iterations % self.config.save_interval == 0:
                 self.save_checkpoint()
             eso = self.eval_step() if (self.config.eval_interval and self.context.iterations % self.config.eval_interval == 0) else None
@@ -256,9 +360,4 @@ class DeterminedBaseTrainer(BaseTrainer[DeterminedBaseContextGeneric, ParallelMo
                 m = self.log_metrics(tso, eso)
                 if return_metrics:
                     out.append(m)
-            if ctx.preempt.should_preempt():
-                self.save_checkpoint()
-                if os.environ.get("DETERMINED_TEST") != "True":
-                    raise SystemExit(0)
-                break
         return out if return_metrics else None

@@ -166,7 +166,10 @@ def test_chat_finetuning_softprompt(tmp_path, mp, pp, world):
     assert any((s2[k] != s4[k]).any() for k in s2)
 
 
-@needs_fixtures
+# tensors-only fixture of the reference test (copied so the GPU box, which has no reference tree, can run it)
+BACKCOMPAT = Path(__file__).resolve().parent / "files" / "backward_compatibility_checkpoint"
+
+
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 def test_backward_compatibility_with_legacy_checkpoint(device):
     """Reference test_backwards_compatibility.py: a legacy (pre-`scaling`) 1-layer checkpoint loaded into the
@@ -177,7 +180,7 @@ def test_backward_compatibility_with_legacy_checkpoint(device):
     from scaling_amd.transformer.data.utils import get_cumulative_seq_lengths, get_position_ids
     from scaling_amd.transformer.model.model import get_transformer_layer_specs
 
-    d = FILES / "backward_compatibility_checkpoint"
+    d = BACKCOMPAT
     sd = torch.load(str(d / "state_dict.pt"), weights_only=True)
     gt = torch.load(str(d / "ground_truth.pt"), weights_only=True)
     arch = TransformerArchitectureConfig(vocab_size=512, sequence_length=4, hidden_size=16, num_attention_heads=2,
