@@ -10,6 +10,7 @@ import sys
 from pathlib import Path
 from typing import Any, Optional
 
+from ..utils.debug_env import debug_env
 from .launch_config import encode_base64
 from .runner_config import RunnerConfig, RunnerType
 
@@ -55,8 +56,10 @@ def get_resource_pool(config: RunnerConfig) -> dict[str, list[int]]:
     return {"localhost": list(range(n))}
 
 
-def _exports() -> dict[str, str]:
+def _exports(config: Optional[RunnerConfig] = None) -> dict[str, str]:
     env = {k: v for k, v in os.environ.items() if any(k.startswith(p) for p in EXPORT_ENVS)}
+    if config is not None:
+        env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking))
     extra = Path.home() / ".deepspeed_env"
     if extra.is_file():
         for line in extra.read_text().splitlines():
@@ -80,7 +83,7 @@ class PDSHRunner:
         local_only = all(h in ("localhost", "127.0.0.1") for h in self.pool)
         if local_only:
             return launch + ["--node_rank=0"] + script
-        exports = " ".join(f"export {k}={v};" for k, v in _exports().items())
+        exports = " ".join(f"export {k}={v};" for k, v in _exports(self.config).items())
         inner = " ".join(launch + ["--node_rank=%n"] + script)
         if self.config.runner_type == RunnerType.PDSH_DOCKER:
             d = self.config.docker_config
@@ -105,6 +108,7 @@ def runner_main(config: RunnerConfig, payload: Optional[dict[str, Any]] = None) 
     cmd = PDSHRunner(config, pool, master).get_cmd(payload)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking))
     proc = subprocess.Popen(cmd, env=env)
     rc = proc.wait()
     if rc != 0:  # the failing rank already printed its error; propagate the code quietly

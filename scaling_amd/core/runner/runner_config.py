@@ -28,3 +28,7 @@ class RunnerConfig(BaseConfig, populate_by_name=True):
     default_gpu_count: int = Field(8, description="GPUs per node if not given in the hosts' slots")
     docker_config: RunnerDockerConfig = Field(RunnerDockerConfig(), description="docker runner configuration")
     use_determined: bool = Field(False, description="use Determined for metric and checkpoint tracking")
+    debug_collectives: bool = Field(False, description="export RCCL/torch.distributed debug logging to every rank")
+    debug_hip_launch_blocking: bool = Field(
+        False, description="export HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL: synchronous, serialized kernel launches"
+    )

@@ -1,0 +1,47 @@
+"""Environment switches for deterministic runs and for debugging collectives / HIP launches
+(SURVEY §5.2 MI355X plan).  The runner exports them to every rank; ``apply`` sets them in-process
+before the first HIP / RCCL call."""
+from __future__ import annotations
+
+import os
+from typing import Mapping
+
+# RCCL honours the NCCL_* names; TORCH_* are torch.distributed's own switches
+COLLECTIVE_DEBUG_ENV: Mapping[str, str] = {
+    "NCCL_DEBUG": "INFO",
+    "NCCL_DEBUG_SUBSYS": "INIT,COLL,P2P",
+    "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1",
+    "TORCH_NCCL_DUMP_ON_TIMEOUT": "1",
+    "TORCH_DISTRIBUTED_DEBUG": "DETAIL",
+}
+
+# every kernel launch synchronous and serialized, so a fault is reported at the launch that caused it
+HIP_LAUNCH_DEBUG_ENV: Mapping[str, str] = {
+    "HIP_LAUNCH_BLOCKING": "1",
+    "AMD_SERIALIZE_KERNEL": "3",
+    "AMD_SERIALIZE_COPY": "3",
+}
+
+# library-side determinism: rocBLAS without atomics, no online GEMM re-tuning (TunableOp only reads its
+# fixed solution table, so every run picks the same kernels); the package's own HIP kernels reduce in a
+# fixed order (no float atomics)
+DETERMINISTIC_ENV: Mapping[str, str] = {
+    "CUBLAS_WORKSPACE_CONFIG": ":4096:8",
+    "ROCBLAS_DEFAULT_ATOMICS_MODE": "0",
+    "PYTORCH_TUNABLEOP_TUNING": "0",
+}
+
+
+def debug_env(collectives: bool = False, hip_launch_blocking: bool = False) -> dict[str, str]:
+    env: dict[str, str] = {}
+    if collectives:
+        env.update(COLLECTIVE_DEBUG_ENV)
+    if hip_launch_blocking:
+        env.update(HIP_LAUNCH_DEBUG_ENV)
+    return env
+
+
+def apply(env: Mapping[str, str], override: bool = False) -> None:
+    for k, v in env.items():
+        if override or k not in os.environ:
+            os.environ[k] = v

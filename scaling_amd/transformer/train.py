@@ -173,8 +173,10 @@ def _init_transformer_config(launch_config: LaunchConfig, overwrite_config: Opti
 
 def _enable_deterministic_torch() -> None:
     # the HIP kernels of this package are deterministic by construction (no atomics in reductions);
-    # this pins down the torch/hipBLASLt side
-    os.environ.setdefault("CUBLAS_WORKSPACE_CONFIG", ":4096:8")
+    # this pins down the torch / rocBLAS / hipBLASLt (TunableOp) side
+    from ..core.utils.debug_env import DETERMINISTIC_ENV, apply
+
+    apply(DETERMINISTIC_ENV)
     torch.use_deterministic_algorithms(True)
 
 

@@ -59,3 +59,23 @@ def test_runner_config_legacy_hostfile_alias(tmp_path):
     hf.write_text("localhost")
     c = RunnerConfig.from_dict({"hostfile": str(hf), "script": str(SCRIPT)})
     assert str(c.hostsfile) == str(hf)
+
+
+def test_runner_debug_and_determinism_env(monkeypatch):
+    from scaling_amd.core.runner.runner import PDSHRunner, _exports
+    from scaling_amd.core.runner.runner_config import RunnerConfig
+    from scaling_amd.core.utils import debug_env
+
+    cfg = RunnerConfig(hosts=["worker-0 slots=0,1", "worker-1 slots=0,1"], debug_collectives=True,
+                       debug_hip_launch_blocking=True, script="train.py")
+    env = _exports(cfg)
+    assert env["NCCL_DEBUG"] == "INFO" and env["HIP_LAUNCH_BLOCKING"] == "1" and env["AMD_SERIALIZE_KERNEL"] == "3"
+    cmd = PDSHRunner(cfg, {"worker-0": [0, 1], "worker-1": [0, 1]}, "10.0.0.1").get_cmd()
+    assert "export NCCL_DEBUG=INFO;" in cmd[-1] and "export HIP_LAUNCH_BLOCKING=1;" in cmd[-1]
+    assert "NCCL_DEBUG" not in _exports(RunnerConfig(hosts=["localhost"]))
+    for k in debug_env.DETERMINISTIC_ENV:  # registered with monkeypatch: restored after the test
+        monkeypatch.delenv(k, raising=False)
+    debug_env.apply(debug_env.DETERMINISTIC_ENV)
+    import os
+
+    assert os.environ["ROCBLAS_DEFAULT_ATOMICS_MODE"] == "0" and os.environ["PYTORCH_TUNABLEOP_TUNING"] == "0"
