@@ -250,6 +250,21 @@ void cast_scale_(const at::Tensor& x, at::Tensor y, double scale) {
     sa_launch::cast_scale(dt(x), dt(y), x.data_ptr(), y.data_ptr(), x.numel(), (float)scale, cur_stream());
 }
 
+// ------------------------------------------------------------------ transpose (dgrad weight cache)
+// out = x^T for a 2-D bf16 / fp16 matrix with unit inner stride (R, C multiples of 64); returns false if the
+// operands are not supported so the caller can fall back
+bool transpose_ok(const at::Tensor& x) {
+    return x.is_cuda() && x.dim() == 2 && x.element_size() == 2 && x.stride(1) == 1 &&
+           (uintptr_t)x.data_ptr() % 16 == 0 && sa_launch::transpose_supported(x.size(0), x.size(1), x.stride(0));
+}
+at::Tensor transpose2d(const at::Tensor& x) {
+    TORCH_CHECK(transpose_ok(x), "transpose2d: 2-byte 2-D cuda tensor, unit inner stride, dims multiple of 64");
+    const at::DeviceGuard g(x.device());
+    auto out = at::empty({x.size(1), x.size(0)}, x.options());
+    sa_launch::transpose_u16(x.data_ptr(), x.stride(0), out.data_ptr(), x.size(0), x.size(1), cur_stream());
+    return out;
+}
+
 // ------------------------------------------------------------------ GEMM (weight gradient)
 // C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
 bool gemm_tn_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
@@ -458,6 +473,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
     m.def("gemm_set_variant", &sa_launch::gemm_set_variant, "select the gemm_tn pipeline variant (benchmarking)");
     m.def("gemm_tn_timing", &gemm_tn_timing, "profiling: per-phase s_memtime stamps of gemm_tn workgroup 0");
+    m.def("transpose_ok", &transpose_ok, "whether transpose2d supports this tensor");
+    m.def("transpose2d", &transpose2d, "x^T (contiguous) for 2-byte 2-D matrices");
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
     m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());

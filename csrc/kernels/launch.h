@@ -43,6 +43,8 @@ int sumsq_blocks(int64_t n);
 void sumsq(int dtype, const void* x, int64_t n, float scale, float* part_sq, float* part_bad, float* out_sq,
            float* out_bad, int accumulate, hipStream_t st);
 void cast_scale(int sdt, int ddt, const void* x, void* y, int64_t n, float scale, hipStream_t st);
+bool transpose_supported(int64_t R, int64_t C, int64_t ld_in);
+void transpose_u16(const void* in, int64_t ld_in, void* out, int64_t R, int64_t C, hipStream_t st);
 }  // namespace sa_launch
 
 namespace sa_launch {

@@ -25,6 +25,7 @@ from ...topology import Topology
 from ..linear import ColumnParallelLinear, RowParallelLinear
 from ..linear.fused import fused_column_linear
 from ..linear.utils import all_concat, all_reduce_scatter_to_sequence_parallel, all_shard
+from ..linear.main_grad import invalidate_transposed_weights
 from ..lora import ParallelLoRa
 from ..lora_config import LoRaConfig, LoRAModuleType
 from ..masked_softmax import MaskedSoftmax, MaskedSoftmaxConfig, MaskedSoftmaxKernel
@@ -459,3 +460,4 @@ class ParallelSelfAttention(torch.nn.Module):
             self.dense.weight.data += self.lora_modules[f"dense_{self.lora_config.name}"].get_delta_weights().to(self.dtype)
         del self.lora_modules
         self.lora_merged_state = True
+        invalidate_transposed_weights()

@@ -17,14 +17,46 @@ gradient's columns before the weight-gradient GEMM, so both gradient paths honou
 Several weights that read the same input (q/k/v, SwiGLU ``dense_in``/``siglu_weight``) run as ONE
 GEMM.  When the weights (and their gradients) sit back to back in the flat buffers the combined
 ``[sum N, K]`` matrix is a zero-copy strided view; otherwise it is concatenated.
+
+Input gradient ``dX = dY W``: hipBLASLt runs that NN layout at ~1.3 PF/s on gfx950 but the forward's
+``X W^T`` layout at ~1.6 PF/s.  With a transposed copy ``W^T`` the backward is ``dY (W^T)^T`` — the forward
+layout — so training keeps a transposed copy of every weight (LDS-tiled transpose kernel, ~12 GB for the 7B
+model), built once per weight update and reused by every micro-batch.  The copies are keyed by a global
+weights generation that the optimizer step, checkpoint loads and LoRA merges advance
+(``invalidate_transposed_weights``); ``SCALING_AMD_DGRAD_WT=0`` turns the cache off.
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Optional, Sequence
 
 import torch
 
-from ....ops.gemm import wgrad
+from ....ops.gemm import transpose2d, wgrad
+
+_GEN = [0]
+_WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
+
+
+def invalidate_transposed_weights() -> None:
+    """Marks every cached W^T stale (call after any in-place change of linear weights)."""
+    _GEN[0] += 1
+
+
+def _transposed(weights: Sequence[torch.Tensor], w: torch.Tensor) -> Optional[torch.Tensor]:
+    """Cached contiguous ``w^T`` ([K, sum N]) for the dgrad GEMM, or None where it does not pay."""
+    if not (_WT_ENABLED and w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2):
+        return None
+    if w.shape[0] % 64 or w.shape[1] % 64 or w.numel() < (1 << 20):
+        return None
+    key = weights[0]
+    c = getattr(key, "_sa_wt_cache", None)
+    if c is not None and c[0] == _GEN[0] and c[1] == len(weights) and c[2].shape == (w.shape[1], w.shape[0]):
+        return c[2]
+    with torch.no_grad():
+        wt = transpose2d(w.detach())
+    key._sa_wt_cache = (_GEN[0], len(weights), wt)  # type: ignore[attr-defined]
+    return wt
 
 
 def _adjacent(ts: Sequence[Optional[torch.Tensor]]) -> Optional[torch.Tensor]:
@@ -57,7 +89,8 @@ def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]
 
 class _MultiLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, n: int, *params: Optional[torch.Tensor]) -> torch.Tensor:  # type: ignore[override]
+    def forward(ctx: Any, x: torch.Tensor, n: int, want_wt: bool,  # type: ignore[override]
+                *params: Optional[torch.Tensor]) -> torch.Tensor:
         weights = params[:n]
         biases = params[n:]
         w = _adjacent(weights)
@@ -68,7 +101,9 @@ class _MultiLinear(torch.autograd.Function):
         if has_bias:
             b = biases[0] if n == 1 else torch.cat(biases, dim=0)  # type: ignore[arg-type]
         out = torch.nn.functional.linear(x, w, b)
-        ctx.save_for_backward(x, w, *weights)
+        wt = _transposed(weights, w) if want_wt else None
+        ctx.has_wt = wt is not None
+        ctx.save_for_backward(x, wt if wt is not None else w, *weights)
         ctx.n, ctx.has_bias = n, has_bias
         ctx.splits = [t.shape[0] for t in weights]  # type: ignore[union-attr]
         return out
@@ -77,9 +112,11 @@ class _MultiLinear(torch.autograd.Function):
     def backward(ctx: Any, g: torch.Tensor):  # type: ignore[override]
         x, w, *weights = ctx.saved_tensors
         n = ctx.n
-        dx = torch.matmul(g, w) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(g, w.t()) if ctx.has_wt else torch.matmul(g, w)  # w is W^T [K, N] with the cache
         dws: list[Optional[torch.Tensor]] = [None] * n
-        if any(ctx.needs_input_grad[2 : 2 + n]):
+        if any(ctx.needs_input_grad[3 : 3 + n]):
             g2 = g.reshape(-1, g.shape[-1])
             x2 = x.reshape(-1, x.shape[-1])
             masks = [getattr(wt, "_sa_grad_row_mask", None) for wt in weights]
@@ -101,19 +138,21 @@ class _MultiLinear(torch.autograd.Function):
         if ctx.has_bias:
             gb = g.reshape(-1, g.shape[-1]).sum(0)
             dbs = list(torch.split(gb, ctx.splits, dim=0)) if n > 1 else [gb]
-        return (dx, None, *dws, *dbs)
+        return (dx, None, None, *dws, *dbs)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``F.linear`` with GEMM-fused gradient accumulation for main-grad weights."""
+    want_wt = torch.is_grad_enabled() and x.requires_grad
     if bias is None:
-        return _MultiLinear.apply(x, 1, weight)
-    return _MultiLinear.apply(x, 1, weight, bias)
+        return _MultiLinear.apply(x, 1, want_wt, weight)
+    return _MultiLinear.apply(x, 1, want_wt, weight, bias)
 
 
 def multi_linear(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Optional[Sequence[Optional[torch.Tensor]]] = None
                  ) -> torch.Tensor:
     """``x @ [W_1; ...; W_n]^T (+ [b_1; ...; b_n])`` as one GEMM (forward, dgrad and wgrad)."""
+    want_wt = torch.is_grad_enabled() and x.requires_grad
     if biases is None or any(b is None for b in biases):
-        return _MultiLinear.apply(x, len(weights), *weights)
-    return _MultiLinear.apply(x, len(weights), *weights, *biases)
+        return _MultiLinear.apply(x, len(weights), want_wt, *weights)
+    return _MultiLinear.apply(x, len(weights), want_wt, *weights, *biases)

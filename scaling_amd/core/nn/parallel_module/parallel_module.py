@@ -23,6 +23,7 @@ from ...optimizer.base import BaseOptimizer
 from ...profiler import Profiler, ProfilerConfig
 from ...topology import Topology
 from ...topology.topology_config import ActivationCheckpointingType
+from ..linear.main_grad import invalidate_transposed_weights
 from ..parameter_meta import CoreParameterMeta
 from ..pipeline_schedule import PipelineScheduleInference, PipelineScheduleTrain
 from ..pipeline_schedule.instructions import (
@@ -167,6 +168,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         return out
 
     def broadcast_model(self) -> None:
+        invalidate_transposed_weights()
         topo = self.topology
         if topo is None or not topo.is_distributed_initialized:
             return
@@ -258,6 +260,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         self._layers.train()
         self.pipe_buffer.reset()
         self.profiler.step()
+        invalidate_transposed_weights()  # weights may have been changed in place since the last step
         if self._param_sync_optimizer is not optimizer:
             optimizer.attach_param_sync(self._layers)
             self._param_sync_optimizer = optimizer

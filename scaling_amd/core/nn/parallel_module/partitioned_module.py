@@ -17,6 +17,7 @@ import torch
 from ...logging import logger
 from ...topology import PipePartitionMethod
 from ...utils.param_merge import merge_parameter, split_parameter
+from ..linear.main_grad import invalidate_transposed_weights
 from ..parameter_meta import CoreParameterMeta
 from .layer_spec import LayerSpec, TiedLayerSpec
 from .pipeline_partitioning import (
@@ -192,6 +193,7 @@ class PipePartitionedModule(torch.nn.Module):
             res = layer.load_state_dict(sd, strict=False)
             missing.update(res.missing_keys)
             unexpected.update(res.unexpected_keys)
+        invalidate_transposed_weights()
         bad_unexpected = {k for k in unexpected if not key_match(k, allowed_unexpected)}
         if unexpected - bad_unexpected:
             logger.warning(f"Ignoring unexpected keys in checkpoint: {unexpected - bad_unexpected}")

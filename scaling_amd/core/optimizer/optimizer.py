@@ -32,6 +32,7 @@ import torch.distributed as dist
 
 from ...ops import optim as optim_ops
 from ..logging import logger
+from ..nn.linear.main_grad import invalidate_transposed_weights
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
 from ..utils.safe_load import safe_load
@@ -300,6 +301,7 @@ class Optimizer(BaseOptimizer):
                     self._gather_bucket(g, gi, b)
             learning_rates[g.config.name or f"parameter_group_{gi}"] = g.lr
         self.zero_grad()
+        invalidate_transposed_weights()
         return OptimizerStepOutput(global_grad_norm, None, learning_rates, ls_out.overflow, ls_out.no_overflow_steps,
                                    ls_out.current_loss_scale, debug_dict)
 
@@ -327,6 +329,7 @@ class Optimizer(BaseOptimizer):
 
     def refresh_optimizer_after_model_change(self) -> None:
         self.wait_param_sync()
+        invalidate_transposed_weights()
         for g in self.parameter_groups:
             g.refresh_optimized_params(self.topology)
 
@@ -486,4 +489,5 @@ class Optimizer(BaseOptimizer):
                 g.adam_step = int(steps[0])
             if gi < len(first["optimizer_param_groups"]):
                 g.lr = first["optimizer_param_groups"][gi].get("lr", g.lr)
+        invalidate_transposed_weights()
         logger.info("loaded optimizer checkpoint")

@@ -27,3 +27,10 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None,
     if accumulate:
         return out.addmm_(dy.t(), x)
     return torch.matmul(dy.t(), x, out=out)
+
+
+def transpose2d(x: torch.Tensor) -> torch.Tensor:
+    """Contiguous ``x^T`` of a 2-D matrix (LDS-tiled HIP kernel for bf16/fp16 at multiples of 64)."""
+    if use_native(x) and ext().transpose_ok(x):
+        return ext().transpose2d(x)
+    return x.t().contiguous()

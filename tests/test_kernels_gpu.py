@@ -554,3 +554,35 @@ def test_dropout_add(dtype, with_res):
     torch.testing.assert_close(x.grad.float(), torch.where(kept, g / 0.7, 0.0).float(), atol=1e-2, rtol=1e-2)
     if with_res:
         assert torch.equal(res.grad, g)
+
+
+@pytest.mark.parametrize("R,C,ld", [(64, 64, 64), (4096, 6144, 6144), (11008, 4096, 4096), (128, 192, 256)])
+def test_transpose2d(R, C, ld):
+    from scaling_amd.ops.gemm import transpose2d
+
+    base = torch.randn(R, ld, device=DEV, dtype=torch.bfloat16)
+    x = base[:, :C]
+    assert ext().transpose_ok(x)
+    assert torch.equal(transpose2d(x), x.t().contiguous())
+
+
+def test_linear_dgrad_with_transposed_weight_cache():
+    """dX through the cached W^T (forward-layout GEMM) equals dX = dY W; the cache follows weight updates."""
+    from scaling_amd.core.nn.linear import main_grad as mg
+
+    torch.manual_seed(0)
+    w = [torch.randn(n, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True) for n in (1024, 256, 256)]
+    x = torch.randn(2, 512, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn(2, 512, 1536, device=DEV, dtype=torch.bfloat16)
+    mg.invalidate_transposed_weights()
+    mg.multi_linear(x, w).backward(g)
+    assert getattr(w[0], "_sa_wt_cache", None) is not None  # the cached path ran
+    ref = g.float() @ torch.cat(w, 0).detach().float()
+    torch.testing.assert_close(x.grad.float(), ref, atol=0.5, rtol=2e-2)
+    with torch.no_grad():
+        w[1].mul_(-1.0)
+    mg.invalidate_transposed_weights()
+    x.grad = None
+    mg.multi_linear(x, w).backward(g)
+    ref2 = g.float() @ torch.cat(w, 0).detach().float()
+    torch.testing.assert_close(x.grad.float(), ref2, atol=0.5, rtol=2e-2)
