@@ -331,6 +331,10 @@ def _worker(a: argparse.Namespace) -> None:
             with open(a.profile_json, "w") as f:
                 json.dump({"per_step_s": per_step, **res}, f)
         print(json.dumps(res), flush=True)
+    if gemm_mode == "tune":
+        from scaling_amd.utils.gemm_tuning import write_tuning_file
+
+        write_tuning_file()
     dist.barrier()
     dist.destroy_process_group()
     if not dp_agree:
