@@ -10,7 +10,8 @@ TAG=${TAG:-run}
 TICK=$!
 trap 'kill $TICK 2>/dev/null || true' EXIT
 if [ -n "$TESTS" ]; then
-  timeout -k 10 400 python -u -m pytest $TESTS -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
+  timeout -k 10 400 python -u -m pytest $TESTS ${TESTK:+-k "$TESTK"} -m gpu -x -v --timeout 200 --timeout-method thread \
+      > gpurun_out/tests_$TAG.log 2>&1
 fi
 if [ "$TUNE" = "1" ]; then
   timeout -k 10 700 python -u bench.py --steps 1 --warmup 1 --gemm-tuning tune \
