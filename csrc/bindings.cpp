@@ -307,7 +307,7 @@ uint32_t drop_threshold(double p) {
 }
 std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& cu_q,
                                const at::Tensor& cu_k, int64_t max_q, double scale, bool causal, int64_t window,
-                               double p_drop, int64_t seed) {
+                               double p_drop, int64_t seed, int64_t local_heads) {
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
     TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash_attn: q/k/v dtypes differ");
     TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "flash_attn: dropout probability must be in [0, 1)");
@@ -326,6 +326,7 @@ std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const a
     a.v_tok = v.stride(0); a.v_head = v.stride(1); a.o_tok = o.stride(0); a.o_head = o.stride(1); a.lse_stride = T;
     a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
     a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)k.size(1); a.causal = causal ? 1 : 0; a.window = (int)window;
+    a.local_heads = local_heads < 0 ? (int)H : (int)local_heads;
     a.scale_log2 = (float)(scale * 1.4426950408889634);
     a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
     if (T > 0 && a.nseg > 0) sa_launch::fa_fwd(a, (int)D, (int)max_q, q.scalar_type() == at::kHalf, cur_stream());
@@ -335,7 +336,7 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
                                const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_q, const at::Tensor& cu_k,
                                int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window,
                                const c10::optional<at::Tensor>& dq_out, const c10::optional<at::Tensor>& dk_out,
-                               const c10::optional<at::Tensor>& dv_out, double p_drop, int64_t seed) {
+                               const c10::optional<at::Tensor>& dv_out, double p_drop, int64_t seed, int64_t local_heads) {
     // d*_out: write the gradients into caller-provided strided views (e.g. slices of one dQKV buffer)
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(o, "o");
     TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() && o.scalar_type() == q.scalar_type() &&
@@ -365,6 +366,7 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
     a.dv_tok = dv.stride(0); a.dv_head = dv.stride(1); a.lse_stride = T;
     a.cu_q = cu_q.data_ptr<int>(); a.cu_k = cu_k.data_ptr<int>();
     a.nseg = (int)cu_q.numel() - 1; a.Hq = (int)H; a.Hkv = (int)Hk; a.causal = causal ? 1 : 0; a.window = (int)window;
+    a.local_heads = local_heads < 0 ? (int)H : (int)local_heads;
     a.scale = (float)scale; a.scale_log2 = (float)(scale * 1.4426950408889634);
     a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
     // GQA head split of the dK/dV sweep: causal/windowed work is triangular, and with few (kv head, key
@@ -490,6 +492,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
-    m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0);
-    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0);
+    m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);
+    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);
 }

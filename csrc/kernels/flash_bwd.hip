@@ -107,11 +107,13 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     const int off = Lk - Lq;
     const int kw0 = kwg0 + 32 * wave, mykey = kw0 + lk;
     const int klast = min(kwg0 + 127, Lk - 1);
+    // the swept q heads h0 .. h0+grp-1 may mix windowed and global heads: the q range is their union
+    const int wun = (a.window >= 0 && h0 + grp <= a.local_heads) ? a.window : -1;
     int qlo = 0, qhi = Lq;
     if (a.causal) qlo = max(0, kwg0 - off);
-    if (a.window >= 0) {
-        qhi = min(Lq, klast - off + a.window + 1);
-        if (!a.causal) qlo = max(0, kwg0 - off - a.window);
+    if (wun >= 0) {
+        qhi = min(Lq, klast - off + wun + 1);
+        if (!a.causal) qlo = max(0, kwg0 - off - wun);
     }
     qlo = (qlo / QT) * QT;
     const int ntq = qhi > qlo ? (qhi - qlo + QT - 1) / QT : 0;
@@ -158,10 +160,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
         const float* DL = LS + 64;
         const int qt = qlo + (w % ntq) * QT;
+        const int win = (h0 + w / ntq) < a.local_heads ? a.window : -1;
         uint32_t hs = 0;
         if constexpr (DROP) hs = drop_head(a.seed, h0 + w / ntq);
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
-                               (a.window >= 0 && (kw0 < qt + QT - 1 + off - a.window || (!a.causal && kw0 + 31 > qt + off + a.window)));
+                               (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
         f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
@@ -178,9 +181,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         if (need_mask) {
             const int rel = mykey - off - qt - 4 * h;
             if (a.causal) mlo = rel;                  // key <= q + off
-            if (a.window >= 0) {
-                mhi = rel + a.window;                 // key >= q + off - window
-                if (!a.causal) mlo = rel - a.window;  // key <= q + off + window
+            if (win >= 0) {
+                mhi = rel + win;                 // key >= q + off - window
+                if (!a.causal) mlo = rel - win;  // key <= q + off + window
             }
         }
 #pragma unroll
@@ -288,6 +291,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
+    const int win = hq < a.local_heads ? a.window : -1;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     const int off = Lk - Lq;
@@ -295,9 +299,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     const int qlast = min(qwg0 + 127, Lq - 1);
     int khi = Lk;
     if (a.causal) khi = min(Lk, qlast + off + 1);
-    else if (a.window >= 0) khi = min(Lk, qlast + off + a.window + 1);
+    else if (win >= 0) khi = min(Lk, qlast + off + win + 1);
     int klo = 0;
-    if (a.window >= 0) klo = max(0, qwg0 + off - a.window);
+    if (win >= 0) klo = max(0, qwg0 + off - win);
     klo = (klo / 64) * 64;
 
     bf16x8 qf[NKS], df[NKS];
@@ -337,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     auto tile = [&](const char* K, int kt) {
         const char* V = K + TILE;
         const bool need_mask = (kt + 64 > Lk) || (a.causal && kt + 63 > qw0 + off) ||
-                               (a.window >= 0 && (kt < qw0 + 31 + off - a.window || (!a.causal && kt + 63 > qw0 + off + a.window)));
+                               (win >= 0 && (kt < qw0 + 31 + off - win || (!a.causal && kt + 63 > qw0 + off + win)));
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             f32x16 s = f32x16{}, dp = f32x16{};
@@ -352,8 +356,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
                 const int base = kt + 32 * b + 4 * h;
                 hi = Lk - 1 - base;
                 if (a.causal) hi = min(hi, myq + off - base);
-                else if (a.window >= 0) hi = min(hi, myq + off + a.window - base);
-                if (a.window >= 0) low = myq + off - a.window - base;
+                else if (win >= 0) hi = min(hi, myq + off + win - base);
+                if (win >= 0) low = myq + off - win - base;
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {

@@ -26,6 +26,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     const int qt = a.causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
+    const int win = hq < a.local_heads ? a.window : -1;  // per-head window (mixed local/global heads)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, lq = lane & 31;
     const int off = Lk - Lq;  // bottom-right causal alignment
     const int qwg0 = qt * 128;
@@ -36,9 +37,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
     const int qlast = min(qwg0 + 127, Lq - 1);
     int khi = Lk;
     if (a.causal) khi = min(Lk, qlast + off + 1);
-    else if (a.window >= 0) khi = min(Lk, qlast + off + a.window + 1);
+    else if (win >= 0) khi = min(Lk, qlast + off + win + 1);
     int klo = 0;
-    if (a.window >= 0) klo = max(0, qwg0 + off - a.window);
+    if (win >= 0) klo = max(0, qwg0 + off - win);
     klo = (klo / 64) * 64;
 
     // Q fragments (B operand of S^T = K Q^T): lane holds Q[myq][16 ks + 8h .. +7]
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
         }
         // ---- scale + mask (mask only on boundary tiles; wave-uniform decision)
         const bool need_mask = (kt + 64 > Lk) || (a.causal && kt + 63 > qw0 + off) ||
-                               (a.window >= 0 && (kt < qw0 + 31 + off - a.window || (!a.causal && kt + 63 > qw0 + off + a.window)));
+                               (win >= 0 && (kt < qw0 + 31 + off - win || (!a.causal && kt + 63 > qw0 + off + win)));
         float mloc = -INFINITY;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
                     const int key = kt + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * h;
                     bool ok = key < Lk && myq < Lq;
                     if (a.causal) ok = ok && key <= myq + off;
-                    if (a.window >= 0) ok = ok && key >= myq + off - a.window && (a.causal || key <= myq + off + a.window);
+                    if (win >= 0) ok = ok && key >= myq + off - win && (a.causal || key <= myq + off + win);
                     x = ok ? x : -INFINITY;
                 }
                 s[b][r] = x;
@@ -200,15 +201,16 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
     const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
+    const int win = hq < a.local_heads ? a.window : -1;  // per-head window (mixed local/global heads)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
     const int off = Lk - Lq;
     const int qwg0 = qt * C::BM, qw0 = qwg0 + 32 * wave, myq = qw0 + lq;
     const int qlast = min(qwg0 + C::BM - 1, Lq - 1);
     int khi = Lk;
     if (a.causal) khi = min(Lk, qlast + off + 1);
-    else if (a.window >= 0) khi = min(Lk, qlast + off + a.window + 1);
+    else if (win >= 0) khi = min(Lk, qlast + off + win + 1);
     int klo = 0;
-    if (a.window >= 0) klo = max(0, qwg0 + off - a.window);
+    if (win >= 0) klo = max(0, qwg0 + off - win);
     klo = (klo / C::KT) * C::KT;
 
     // ---- per-lane LDS offsets (bytes, relative to a tile base) ----
@@ -268,16 +270,16 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
         }
         // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
         const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
-                               (a.window >= 0 && (kt < qw0 + 31 + off - a.window ||
-                                                  (!a.causal && kt + C::KT - 1 > qw0 + off + a.window)));
+                               (win >= 0 && (kt < qw0 + 31 + off - win ||
+                                                  (!a.causal && kt + C::KT - 1 > qw0 + off + win)));
         if (need_mask) {
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
                 int hi = Lk - 1 - base;
                 if (a.causal) hi = min(hi, myq + off - base);
-                else if (a.window >= 0) hi = min(hi, myq + off + a.window - base);
-                const int lo = a.window >= 0 ? myq + off - a.window - base : -1;
+                else if (win >= 0) hi = min(hi, myq + off + win - base);
+                const int lo = win >= 0 ? myq + off - win - base : -1;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
             }

@@ -63,6 +63,7 @@ struct FwdArgs {
     int64_t q_tok, q_head, k_tok, k_head, v_tok, v_head, o_tok, o_head, lse_stride;
     const int* cu_q; const int* cu_k;
     int nseg, Hq, Hkv, causal, window;
+    int local_heads;  // q heads [0, local_heads) use `window`, the rest attend globally (mixed local/global)
     float scale_log2;
     // attention-probability dropout (p_drop > 0): keep iff mix(seed, q head, q token, k token) >= drop_thr
     float p_drop, rp_drop;  // rp_drop = 1 / (1 - p_drop)
@@ -80,6 +81,7 @@ struct BwdArgs {
     int64_t dq_tok, dq_head, dk_tok, dk_head, dv_tok, dv_head, lse_stride;
     const int* cu_q; const int* cu_k;
     int nseg, Hq, Hkv, causal, window;
+    int local_heads;
     float scale, scale_log2;
     float p_drop, rp_drop;
     uint32_t seed, drop_thr;

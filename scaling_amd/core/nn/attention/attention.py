@@ -308,8 +308,6 @@ class ParallelSelfAttention(torch.nn.Module):
         re = self.rotary_embedding
         if re is None or not self.use_flash_attention or self.key_query_norm:
             return None
-        if nl > 0 and nl != self.num_attention_heads:
-            return None
         if self.lora_config is not None and not self.lora_merged_state:
             return None
         pos = position_ids.reshape(-1) if position_ids is not None else None
@@ -317,7 +315,7 @@ class ParallelSelfAttention(torch.nn.Module):
             base, q, k, v, re.cos_table, re.sin_table, pos, re.dimensions, s, re.interleaved, cumulative_seq_lengths,
             max_seq_length if max_seq_length is not None else s, self.scaling_factor, self.causal,
             self.local_attention_window_size if nl > 0 else None,
-            dropout_p=self.dropout_attention_probs if self.training else 0.0)
+            dropout_p=self.dropout_attention_probs if self.training else 0.0, local_heads=nl if nl > 0 else None)
 
     def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
         assert self.lora_config is not None
@@ -393,16 +391,10 @@ class ParallelSelfAttention(torch.nn.Module):
                 softmax_scale=self.scaling_factor, causal=self.causal, dropout_p=self.dropout_attention_probs,
                 training=self.training,
             )
-            if nl <= 0 or nl == self.num_attention_heads:
-                window = self.local_attention_window_size if nl > 0 else None
-                hidden = attn_ops.flash_attention(q, k, v, window=window, **common)
-            else:
-                rep = self.num_repeat_kv
-                kr, vr = repeat_kv(k, rep), repeat_kv(v, rep)
-                h_loc = attn_ops.flash_attention(q[:, :nl], kr[:, :nl], vr[:, :nl],
-                                                 window=self.local_attention_window_size, **common)
-                h_glob = attn_ops.flash_attention(q[:, nl:], kr[:, nl:], vr[:, nl:], window=None, **common)
-                hidden = torch.cat([h_loc, h_glob], dim=1)
+            # mixed local/global heads: ONE launch, the kernel picks the window per q head (heads [0, nl)
+            # windowed) — no second launch, no repeat_kv (reference attention.py:619-667 runs two)
+            window = self.local_attention_window_size if nl > 0 else None
+            hidden = attn_ops.flash_attention(q, k, v, window=window, local_heads=nl if nl > 0 else None, **common)
             hidden = hidden.reshape(b, s, -1)
         else:
             kr = repeat_kv(k, self.num_repeat_kv).reshape(b, Tk // b, -1, hd)

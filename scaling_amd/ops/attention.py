@@ -67,9 +67,10 @@ def dropout_seed(device: torch.device) -> int:
 
 
 def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p: float = 0.0, training=False,
-                        dropout_seed_value: Optional[int] = None):
+                        dropout_seed_value: Optional[int] = None, local_heads: Optional[int] = None):
     """Dense per-segment fp32 attention (numerical oracle and CPU path). q:[T,Hq,D], k/v:[Tk,Hk,D].
-    With ``dropout_seed_value`` the dropout mask is the fused kernel's (:func:`dropout_keep_mask`)."""
+    With ``dropout_seed_value`` the dropout mask is the fused kernel's (:func:`dropout_keep_mask`).
+    ``local_heads``: only q heads [0, local_heads) use ``window``, the others attend globally."""
     Hq, Hk = q.shape[1], k.shape[1]
     rep = Hq // Hk
     out = torch.empty(q.shape[0], Hq, v.shape[2], dtype=q.dtype, device=q.device)
@@ -88,11 +89,14 @@ def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p
         ok = torch.ones(Lq, Lk, dtype=torch.bool, device=q.device)
         if causal:
             ok &= kpos <= qpos
+        okw = ok.clone()
         if window is not None and window >= 0:
-            ok &= kpos >= qpos - window
+            okw &= kpos >= qpos - window
             if not causal:
-                ok &= kpos <= qpos + window
-        s = s.masked_fill(~ok, float("-inf"))
+                okw &= kpos <= qpos + window
+        nl = Hq if local_heads is None or local_heads < 0 else min(local_heads, Hq)
+        okh = torch.stack([okw if h < nl else ok for h in range(Hq)])  # [H, Lq, Lk]
+        s = s.masked_fill(~okh, float("-inf"))
         p = torch.softmax(s, dim=-1)
         p = torch.nan_to_num(p, nan=0.0)
         if dropout_p > 0 and training:
@@ -109,19 +113,20 @@ def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p
 
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window, p_drop=0.0, seed=0):  # type: ignore[override]
-        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed)
+    def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window, p_drop=0.0, seed=0,  # type: ignore[override]
+                local_heads=-1):
+        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads)
         ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
-        ctx.cfg = (max_q, max_k, scale, causal, window, p_drop, seed)
+        ctx.cfg = (max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         q, k, v, o, lse, cu_q, cu_k = ctx.saved_tensors
-        max_q, max_k, scale, causal, window, p_drop, seed = ctx.cfg
+        max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
         dq, dk, dv = ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, None, None, None,
-                                  p_drop, seed)
-        return dq, dk, dv, None, None, None, None, None, None, None, None, None
+                                  p_drop, seed, local_heads)
+        return dq, dk, dv, None, None, None, None, None, None, None, None, None, None
 
 
 def _spec(t: torch.Tensor, base: torch.Tensor) -> tuple:
@@ -142,32 +147,34 @@ class _RopeFlashAttn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx: Any, base, specs, cos, sin, pos, rot_dim, seq_len, interleaved, cu_q, cu_k, max_q, max_k, scale,
-                causal, window, p_drop=0.0, seed=0):  # type: ignore[override]
+                causal, window, p_drop=0.0, seed=0, local_heads=-1):  # type: ignore[override]
         qi, ki, vi = (_view(base, sp) for sp in specs)
         q = ext().rope(qi, cos, sin, pos, rot_dim, seq_len, interleaved, False)
         k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
-        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed)
+        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads)
         ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
-        ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed)
+        ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
-        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed = ctx.cfg
+        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
         v = _view(base, specs[2])
-        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed)
+        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
+                     local_heads)
         ext().rope(dq, cos, sin, pos, rot_dim, seq_len, interleaved, True, dq)
         ext().rope(dk, cos, sin, pos, rot_dim, seq_len, interleaved, True, dk)
-        return (dbase,) + (None,) * 16
+        return (dbase,) + (None,) * 17
 
 
 def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cos: torch.Tensor,
                          sin: torch.Tensor, pos: Optional[torch.Tensor], rot_dim: int, seq_len: int, interleaved: bool,
                          cu_seqlens: torch.Tensor, max_seqlen: int, softmax_scale: float, causal: bool = True,
-                         window: Optional[int] = None, dropout_p: float = 0.0) -> Optional[torch.Tensor]:
+                         window: Optional[int] = None, dropout_p: float = 0.0,
+                         local_heads: Optional[int] = None) -> Optional[torch.Tensor]:
     """Fused RoPE + flash attention for q/k/v that are views tiling ``base`` exactly (the QKV GEMM output).
 
     Returns None when the fused path does not apply (CPU tensors, layouts that do not tile ``base``); the
@@ -186,7 +193,7 @@ def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v
     seed = dropout_seed(base.device) if dropout_p > 0.0 else 0
     return _RopeFlashAttn.apply(base, specs, cos, sin, p, int(rot_dim), int(seq_len), bool(interleaved), cq, cq,
                                 int(max_seqlen), int(max_seqlen), float(softmax_scale), bool(causal), win,
-                                float(dropout_p), seed)
+                                float(dropout_p), seed, -1 if local_heads is None else int(local_heads))
 
 
 def flash_attention(
@@ -202,8 +209,12 @@ def flash_attention(
     window: Optional[int] = None,
     dropout_p: float = 0.0,
     training: bool = False,
+    local_heads: Optional[int] = None,
 ) -> torch.Tensor:
-    """q: [T, Hq, D]; k, v: [Tk, Hk, D] (unit last stride); cu_seqlens int32 [nseg+1]."""
+    """q: [T, Hq, D]; k, v: [Tk, Hk, D] (unit last stride); cu_seqlens int32 [nseg+1].
+
+    ``local_heads``: with a ``window``, only q heads [0, local_heads) are windowed and the rest attend
+    globally — mixed local/global heads in ONE launch (the kernels pick the window per head)."""
     if cu_seqlens_k is None:
         cu_seqlens_k = cu_seqlens_q
         max_seqlen_k = max_seqlen_q
@@ -221,7 +232,9 @@ def flash_attention(
         if max_seqlen_k is None:
             max_seqlen_k = int((ck[1:] - ck[:-1]).max().item())
         seed = dropout_seed(q.device) if p_drop > 0.0 else 0
+        lh = -1 if local_heads is None else int(local_heads)
         out = _FlashAttn.apply(q, k, v, cq, ck, int(max_seqlen_q), int(max_seqlen_k), float(scale), bool(causal), win,
-                               p_drop, seed)
+                               p_drop, seed, lh)
         return out if out.dtype == in_dtype else out.to(in_dtype)
-    return attention_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, scale, causal, win, dropout_p, training)
+    return attention_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, scale, causal, win, dropout_p, training,
+                               local_heads=local_heads)

@@ -231,3 +231,18 @@ def test_elementwise_cpu_paths_match_torch():
     a = elementwise.dropout_add(x, None, 0.5, training=True)
     torch.manual_seed(0)
     assert torch.equal(a, torch.nn.functional.dropout(x, 0.5, training=True))
+
+
+def test_attention_reference_mixed_local_global_heads_matches_two_calls():
+    """CPU oracle: per-head window (heads [0, nl) local) equals the reference's two-call split."""
+    from scaling_amd.ops.attention import attention_reference
+
+    torch.manual_seed(0)
+    T, Hq, Hk, D, nl, w = 40, 6, 2, 16, 2, 5
+    q, k, v = torch.randn(T, Hq, D), torch.randn(T, Hk, D), torch.randn(T, Hk, D)
+    cu = torch.tensor([0, 25, 40], dtype=torch.int32)
+    both = attention_reference(q, k, v, cu, cu, 0.25, True, w, local_heads=nl)
+    kr, vr = k.repeat_interleave(Hq // Hk, 1), v.repeat_interleave(Hq // Hk, 1)
+    loc = attention_reference(q[:, :nl], kr[:, :nl], vr[:, :nl], cu, cu, 0.25, True, w)
+    glob = attention_reference(q[:, nl:], kr[:, nl:], vr[:, nl:], cu, cu, 0.25, True, -1)
+    torch.testing.assert_close(both, torch.cat([loc, glob], 1))

@@ -342,7 +342,7 @@ def test_sumsq_cast_unaligned(dtype, offset):
     torch.testing.assert_close(y, x.float() * 0.5, equal_nan=True)
 
 
-def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0, p_drop=0.0):
+def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0, p_drop=0.0, local_heads=None):
     torch.manual_seed(seed)
     T = sum(lens)
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device=DEV, dtype=torch.int32)
@@ -353,14 +353,16 @@ def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0,
     scale = 1 / math.sqrt(D)
     if p_drop > 0:
         dseed = 12345 + seed
-        o = attention._FlashAttn.apply(q, k, v, cu, cu, max(lens), max(lens), scale, causal, window, p_drop, dseed)
+        o = attention._FlashAttn.apply(q, k, v, cu, cu, max(lens), max(lens), scale, causal, window, p_drop, dseed,
+                                       -1 if local_heads is None else local_heads)
     else:
         dseed = None
-        o = attention.flash_attention(q, k, v, cu, cu, max(lens), max(lens), scale, causal, None if window < 0 else window)
+        o = attention.flash_attention(q, k, v, cu, cu, max(lens), max(lens), scale, causal, None if window < 0 else window,
+                                      local_heads=local_heads)
     assert o.dtype == dtype
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
     orf = attention.attention_reference(qr, kr, vr, cu, cu, scale, causal, window, dropout_p=p_drop, training=p_drop > 0,
-                                        dropout_seed_value=dseed)
+                                        dropout_seed_value=dseed, local_heads=local_heads)
     torch.testing.assert_close(o.float(), orf, atol=2e-2, rtol=2e-2)
     g = torch.randn_like(o)
     o.backward(g)
@@ -383,6 +385,18 @@ def test_flash_attention_gqa_varlen():
 
 def test_flash_attention_window():
     _attn_case([333, 129], 4, 4, 64, True, window=50)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("local_heads", [1, 3, 6])
+def test_flash_attention_mixed_local_global_heads(causal, local_heads):
+    """One launch with a per-head window: q heads [0, local_heads) windowed, the rest global; GQA groups
+    that mix both kinds (8 q / 2 kv heads) exercise the union q range of the dK/dV sweep."""
+    _attn_case([300, 77], 8, 2, 128, causal, window=40, local_heads=local_heads)
+
+
+def test_flash_attention_mixed_heads_dropout():
+    _attn_case([190, 66], 8, 2, 64, True, window=30, p_drop=0.2, local_heads=3)
 
 
 def test_flash_attention_d32_noncausal_odd():

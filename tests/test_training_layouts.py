@@ -115,14 +115,14 @@ def test_load_checkpoint_non_strict(tmp_path, mp, pp, world):
 
 
 @pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (2, 1, 2)])
-@pytest.mark.parametrize("kernel", ["torch", "flash_attention"])
-def test_local_attention_training(tmp_path, mp, pp, world, kernel):
-    """Reference test_training_local_attention.py: sliding-window heads train (finite losses, bit-exact resume)."""
-    if kernel == "torch":
-        pytest.skip("local attention requires the flash kernel (reference attention.py:319-332)")
+@pytest.mark.parametrize("local_heads", [4, 2])
+def test_local_attention_training(tmp_path, mp, pp, world, local_heads):
+    """Reference test_training_local_attention.py: sliding-window heads train (finite losses, bit-exact resume);
+    local_heads=2 of 4 is the mixed local/global layout (one attention call with a per-head window).  Local
+    attention needs the flash kernel path (reference attention.py:319-332)."""
     _make_data(tmp_path / "data")
-    cfg = _config(tmp_path, mp, pp, world, masked_softmax={"kernel": kernel}, num_local_attention_heads=4,
-                  local_attention_window_size=16)
+    cfg = _config(tmp_path, mp, pp, world, masked_softmax={"kernel": "flash_attention"},
+                  num_local_attention_heads=local_heads, local_attention_window_size=16)
     full = _run(tmp_path, cfg, world, "full")
     assert all(np.isfinite(_losses(full)))
     cfg["trainer"]["assert_checkpoint_loaded"] = True
