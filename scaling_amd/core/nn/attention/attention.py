@@ -208,10 +208,15 @@ class ParallelSelfAttention(torch.nn.Module):
         if num_local_attention_heads > 0:
             assert self.use_flash_attention, "local attention is currently only supported with `flash_attention`."
             assert local_attention_window_size is not None, "`local_attention_window_size` needs to be set"
-            if num_local_attention_heads != num_attention_heads and mp > 1:
-                raise NotImplementedError("Mixed range attention is not supported with tensor parallelism.")
         assert num_attention_heads % mp == 0, "attention heads must be divisible by model parallel size"
         self.num_attention_heads_per_partition = num_attention_heads // mp
+        # heads [0, num_local_attention_heads) of the whole layer are windowed; this TP partition holds heads
+        # [rank * hp, (rank + 1) * hp), so mixed local/global heads also work under tensor parallelism (the
+        # reference raises NotImplementedError there): the kernels take the window per head
+        hp = self.num_attention_heads_per_partition
+        rank = 0 if topology is None or mp == 1 else topology.model_parallel_rank
+        self.num_local_attention_heads_per_partition = (
+            min(max(num_local_attention_heads - rank * hp, 0), hp) if num_local_attention_heads > 0 else 0)
         self.dtype = dtype
         self.qkv_in_one = qkv_in_one
         self.num_kv_heads = num_kv_heads
@@ -315,7 +320,8 @@ class ParallelSelfAttention(torch.nn.Module):
             base, q, k, v, re.cos_table, re.sin_table, pos, re.dimensions, s, re.interleaved, cumulative_seq_lengths,
             max_seq_length if max_seq_length is not None else s, self.scaling_factor, self.causal,
             self.local_attention_window_size if nl > 0 else None,
-            dropout_p=self.dropout_attention_probs if self.training else 0.0, local_heads=nl if nl > 0 else None)
+            dropout_p=self.dropout_attention_probs if self.training else 0.0,
+            local_heads=self.num_local_attention_heads_per_partition if nl > 0 else None)
 
     def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
         assert self.lora_config is not None
@@ -394,7 +400,8 @@ class ParallelSelfAttention(torch.nn.Module):
             # mixed local/global heads: ONE launch, the kernel picks the window per q head (heads [0, nl)
             # windowed) — no second launch, no repeat_kv (reference attention.py:619-667 runs two)
             window = self.local_attention_window_size if nl > 0 else None
-            hidden = attn_ops.flash_attention(q, k, v, window=window, local_heads=nl if nl > 0 else None, **common)
+            hidden = attn_ops.flash_attention(q, k, v, window=window, **common,
+                                              local_heads=self.num_local_attention_heads_per_partition if nl > 0 else None)
             hidden = hidden.reshape(b, s, -1)
         else:
             kr = repeat_kv(k, self.num_repeat_kv).reshape(b, Tk // b, -1, hd)

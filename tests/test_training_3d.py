@@ -82,3 +82,20 @@ def test_parallel_losses_match_single_rank(tmp_path, mp, pp, world, acc, mbs):
         c["trainer"].update(assert_checkpoint_loaded=True, save_dir=None)
         out[key] = _losses(_run(tmp_path, c, w, key))
     np.testing.assert_allclose(out["par"], out["ref"], rtol=1e-5)
+
+
+def test_mixed_local_global_heads_tp2_matches_single_rank(tmp_path):
+    """Heads [0, 2) of 4 windowed, the rest global, split over TP=2 (one partition all local, one all
+    global): resumed losses equal the single-rank run to 1e-5 (the reference has no TP support here)."""
+    _make_data(tmp_path / "data")
+    base = _llama_cfg(tmp_path, 1, 1, 1, acc=2, dropout=False)
+    base["transformer_architecture"].update(num_local_attention_heads=2, local_attention_window_size=16,
+                                            masked_softmax={"kernel": "flash_attention"})
+    _run(tmp_path, base, 1, "pre")
+    out = {}
+    for key, (m, w) in {"ref": (1, 1), "tp2": (2, 2)}.items():
+        c = copy.deepcopy(base)
+        c["topology"].update(world_size=w, model_parallel_size=m)
+        c["trainer"].update(assert_checkpoint_loaded=True, save_dir=None)
+        out[key] = _losses(_run(tmp_path, c, w, key))
+    np.testing.assert_allclose(out["tp2"], out["ref"], rtol=1e-5)
