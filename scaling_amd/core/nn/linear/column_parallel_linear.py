@@ -7,7 +7,7 @@ import torch
 
 from ...topology import Topology
 from ..parameter_meta import CoreParameterMeta
-from .utils import all_concat, copy_to_tensor_model_parallel_region, get_device
+from .utils import all_concat, get_device, tp_input_grad_group
 from .main_grad import linear as main_grad_linear
 
 
@@ -55,9 +55,8 @@ class ColumnParallelLinear(torch.nn.Module):
         return getattr(self, self.bias_name) if self.bias_name is not None else None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.model_parallel_size > 1 and self.topology is not None and not self.topology.config.sequence_parallel:
-            x = copy_to_tensor_model_parallel_region(x, topology=self.topology)
-        out = main_grad_linear(x, self.weight, self.bias_param)
+        # copy_to region folded into the linear: its input-gradient all-reduce overlaps the wgrad GEMM
+        out = main_grad_linear(x, self.weight, self.bias_param, tp_group=tp_input_grad_group(self.topology))
         if self.parallel_output or self.topology is None:
             return out
         return all_concat(out, dim=-1, topology=self.topology)

@@ -14,16 +14,13 @@ from typing import Any, Sequence
 import torch
 
 from .main_grad import multi_linear
-from .utils import copy_to_tensor_model_parallel_region
+from .utils import tp_input_grad_group
 
 
 def fused_column_linear(x: torch.Tensor, modules: Sequence[torch.nn.Module], topology: Any) -> torch.Tensor:
     """Apply several ColumnParallelLinear (parallel_output=True) modules to the same input with one GEMM."""
-    tp = 1 if topology is None else topology.config.model_parallel_size
-    if tp > 1 and not topology.config.sequence_parallel:
-        x = copy_to_tensor_model_parallel_region(x, topology=topology)
     weights = [m.weight for m in modules]  # type: ignore[attr-defined]
     biases = [getattr(m, "bias_param", None) for m in modules]
     if any(b is None for b in biases):
         biases = [None] * len(modules)
-    return multi_linear(x, weights, biases)
+    return multi_linear(x, weights, biases, tp_group=tp_input_grad_group(topology))

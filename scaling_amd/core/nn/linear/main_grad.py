@@ -18,6 +18,13 @@ Several weights that read the same input (q/k/v, SwiGLU ``dense_in``/``siglu_wei
 GEMM.  When the weights (and their gradients) sit back to back in the flat buffers the combined
 ``[sum N, K]`` matrix is a zero-copy strided view; otherwise it is concatenated.
 
+Tensor parallelism (column-parallel weights without sequence parallelism): the input gradient must be
+summed over the TP group.  Instead of a separate ``copy_to`` region whose all-reduce runs after the whole
+linear backward, the Function takes the TP group and issues the all-reduce of ``dX`` asynchronously right
+after the dgrad GEMM, runs the weight-gradient GEMM while RCCL moves ``dX`` over xGMI, and waits only
+before returning (Megatron's async TP all-reduce; the reference runs them back to back,
+``column_parallel_linear.py:137-139``).
+
 Input gradient ``dX = dY W``: hipBLASLt runs that NN layout at ~1.3 PF/s on gfx950 but the forward's
 ``X W^T`` layout at ~1.6 PF/s.  With a transposed copy ``W^T`` the backward is ``dY (W^T)^T`` — the forward
 layout — so training keeps a transposed copy of every weight (LDS-tiled transpose kernel, ~12 GB for the 7B
@@ -31,6 +38,7 @@ import os
 from typing import Any, Optional, Sequence
 
 import torch
+import torch.distributed as dist
 
 from ....ops.gemm import transpose2d, wgrad
 
@@ -89,7 +97,7 @@ def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]
 
 class _MultiLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx: Any, x: torch.Tensor, n: int, want_wt: bool,  # type: ignore[override]
+    def forward(ctx: Any, x: torch.Tensor, n: int, want_wt: bool, tp_group: Any,  # type: ignore[override]
                 *params: Optional[torch.Tensor]) -> torch.Tensor:
         weights = params[:n]
         biases = params[n:]
@@ -104,7 +112,7 @@ class _MultiLinear(torch.autograd.Function):
         wt = _transposed(weights, w) if want_wt else None
         ctx.has_wt = wt is not None
         ctx.save_for_backward(x, wt if wt is not None else w, *weights)
-        ctx.n, ctx.has_bias = n, has_bias
+        ctx.n, ctx.has_bias, ctx.tp_group = n, has_bias, tp_group
         ctx.splits = [t.shape[0] for t in weights]  # type: ignore[union-attr]
         return out
 
@@ -113,10 +121,14 @@ class _MultiLinear(torch.autograd.Function):
         x, w, *weights = ctx.saved_tensors
         n = ctx.n
         dx = None
+        work = None
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(g, w.t()) if ctx.has_wt else torch.matmul(g, w)  # w is W^T [K, N] with the cache
+            if ctx.tp_group is not None:  # TP input-gradient all-reduce overlapped with the wgrad GEMM below
+                dx = dx.contiguous()
+                work = dist.all_reduce(dx, group=ctx.tp_group, async_op=True)
         dws: list[Optional[torch.Tensor]] = [None] * n
-        if any(ctx.needs_input_grad[3 : 3 + n]):
+        if any(ctx.needs_input_grad[4 : 4 + n]):
             g2 = g.reshape(-1, g.shape[-1])
             x2 = x.reshape(-1, x.shape[-1])
             masks = [getattr(wt, "_sa_grad_row_mask", None) for wt in weights]
@@ -138,21 +150,25 @@ class _MultiLinear(torch.autograd.Function):
         if ctx.has_bias:
             gb = g.reshape(-1, g.shape[-1]).sum(0)
             dbs = list(torch.split(gb, ctx.splits, dim=0)) if n > 1 else [gb]
-        return (dx, None, None, *dws, *dbs)
+        if work is not None:
+            work.wait()
+        return (dx, None, None, None, *dws, *dbs)
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear`` with GEMM-fused gradient accumulation for main-grad weights."""
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, tp_group: Any = None
+           ) -> torch.Tensor:
+    """``F.linear`` with GEMM-fused gradient accumulation for main-grad weights; ``tp_group``: all-reduce the
+    input gradient over it (column-parallel weight, identity forward), overlapped with the wgrad GEMM."""
     want_wt = torch.is_grad_enabled() and x.requires_grad
     if bias is None:
-        return _MultiLinear.apply(x, 1, want_wt, weight)
-    return _MultiLinear.apply(x, 1, want_wt, weight, bias)
+        return _MultiLinear.apply(x, 1, want_wt, tp_group, weight)
+    return _MultiLinear.apply(x, 1, want_wt, tp_group, weight, bias)
 
 
-def multi_linear(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Optional[Sequence[Optional[torch.Tensor]]] = None
-                 ) -> torch.Tensor:
+def multi_linear(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Optional[Sequence[Optional[torch.Tensor]]] = None,
+                 tp_group: Any = None) -> torch.Tensor:
     """``x @ [W_1; ...; W_n]^T (+ [b_1; ...; b_n])`` as one GEMM (forward, dgrad and wgrad)."""
     want_wt = torch.is_grad_enabled() and x.requires_grad
     if biases is None or any(b is None for b in biases):
-        return _MultiLinear.apply(x, len(weights), want_wt, *weights)
-    return _MultiLinear.apply(x, len(weights), want_wt, *weights, *biases)
+        return _MultiLinear.apply(x, len(weights), want_wt, tp_group, *weights)
+    return _MultiLinear.apply(x, len(weights), want_wt, tp_group, *weights, *biases)

@@ -15,4 +15,5 @@ from ....parallel.tp import (  # noqa: F401
     raw_gather_seq,
     raw_reduce_scatter_seq,
     raw_shard,
+    tp_input_grad_group,
 )

@@ -157,6 +157,16 @@ def gather_from_sequence_parallel_region(
     return _Region.apply(x, lambda t: raw_gather_seq(t, size, group), lambda g: raw_reduce_scatter_seq(g, size, group))
 
 
+def tp_input_grad_group(topology: Any) -> Any:
+    """The TP group whose sum a column-parallel linear's input gradient needs (the ``copy_to`` region's
+    backward), or None: tp == 1, sequence parallelism (the gather region in front of the linear reduces
+    instead), or no process group."""
+    size, _, group = _tp(topology)
+    if size == 1 or topology.config.sequence_parallel:
+        return None
+    return group
+
+
 def get_device(topology: Any = None, device: torch.device | None = None) -> torch.device:
     assert topology is None or device is None, "cannot specify both device and topology"
     if topology is not None:
