@@ -353,6 +353,168 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Variant 4: the same ping-pong pipeline (BK 64, two stages, group 0 stages A images, group 1 stages B images in its
+// MFMA window) on v_mfma_f32_16x16x32_bf16 — 64 MFMAs of 16 cycles per K-tile per wave instead of 32 of 32 cycles:
+// the same cycles per FLOP, but the chip holds a higher clock on the 16x16 shape on random data
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7).
+//  * fragment: lane (g = lane>>4, i = lane&15) holds column c0+i of the operand with k rows
+//    {kb+4g .. +3} and {kb+16+4g .. +3} (two ds_read_b64_tr_b16); A and B use the same k permutation;
+//  * the four 16-lane groups read the SAME 16 columns at different k rows, so the image swizzle also separates
+//    rows r and r+4: 16-B slot ^ ((r&3)<<2 ^ ((r>>2)&1)<<1) keeps every half-wave's 32 8-B reads in 16 distinct
+//    16-B bank windows (conflict-free); the LDS-DMA source addresses carry the same permutation.
+__device__ __forceinline__ int sw16(int r) { return ((r & 3) << 2) ^ (((r >> 2) & 1) << 1); }
+__device__ __forceinline__ int koff16(int r, int c) { return r * 512 + 16 * ((c >> 3) ^ sw16(r)) + ((c & 7) << 1); }
+
+__device__ __forceinline__ bf16x8 frag16_tr(const char* img, int kb, int c0, int lane) {
+    const int g = lane >> 4, i = lane & 15;
+    const int row = kb + 4 * g + (i >> 2);
+    const int col = c0 + 4 * (i & 3);
+    const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + koff16(row, col)));
+    const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + koff16(row + 16, col)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int NP, int NW>
+struct Dma16 : Dma<NP, NW> {
+    __device__ __forceinline__ void init(int wave, int lane, int ld) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const int piece = wave + NW * i;
+            const int row = 2 * piece + (lane >> 5);
+            const int slot = (lane & 31) ^ sw16(row);
+            this->voff[i] = (row * ld + slot * 8) * 2;
+        }
+    }
+};
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool BETA>
+__global__ __launch_bounds__(512, 1) void gemm_tn16_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                           const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                           u16* __restrict__ C, int ldc, int M, int N, int K) {
+    constexpr int BK = 64;
+    using G = Cfg<BK>;
+    constexpr int KS = BK / 32;                  // 16x16x32 k-steps per K-tile
+    constexpr int NW = kWaves / 2;               // waves staging one image
+    constexpr int NP = G::kImg / 1024 / NW;      // LDS-DMA instructions per staging wave per image
+    constexpr int NMF = KS * 8 * 4;              // MFMAs per wave per K-tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 2, wn = wave & 3;  // wm doubles as the ping-pong group
+
+    const int tm = M / 256, tn = N / 256, nwg = tm * tn;
+    const int v = xcd_remap(blockIdx.x, nwg);
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    Dma16<NP, NW> da, db;
+    const int swave = wave & 3;
+    da.init(swave, lane, lda);
+    db.init(swave, lane, ldb);
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+#define SA_ISSUE_G(t_)                                                                                        \
+    {                                                                                                         \
+        char* st_ = smem + ((t_) & 1) * G::kStage;                                                            \
+        const int k0_ = (t_) * BK;                                                                            \
+        if (wm == 0) da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave);       \
+        else db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave);     \
+    }
+    SA_ISSUE_G(0)
+    if (wm == 1 && nk > 1) {
+        SA_ISSUE_G(1)
+        wait_vm<NP>();
+    } else {
+        wait_vm<0>();
+    }
+    hard_barrier();
+    if (wm == 1) hard_barrier();
+    for (int t = 0; t < nk; ++t) {
+        const char* ia = smem + (t & 1) * G::kStage;
+        const char* ib = ia + G::kImg;
+        bf16x8 a[KS][8], b[KS][4];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[ks][i] = frag16_tr(ia, 32 * ks, 128 * wm + 16 * i, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[ks][j] = frag16_tr(ib, 32 * ks, 64 * wn + 16 * j, lane);
+        }
+        if (t + 1 < nk) {
+            if (wm == 0) SA_ISSUE_G(t + 1)
+            else wait_vm<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        hard_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        const bool stage_b = wm == 1 && t + 2 < nk;
+        const int soff_b = __builtin_amdgcn_readfirstlane(((t + 2) * BK * ldb + n0) * 2);
+        char* st_b = smem + (t & 1) * G::kStage + G::kImg;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][j] = mfma16(b[ks][j], a[ks][i], acc[i][j]);
+                    constexpr int every = NMF / NP;
+                    const int m = ks * 32 + i * 4 + j;
+                    if (m % every == every - 1 && stage_b) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        db.load_piece(m / every, B, b_bytes, soff_b, st_b, swave);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (wm == 0 && t + 1 < nk) wait_vm<0>();
+        hard_barrier();
+    }
+#undef SA_ISSUE_G
+    if (wm == 0) hard_barrier();  // equal barrier counts for both groups
+
+    // epilogue: acc[i][j][e] = C[m0 + 128wm + 16i + (lane & 15)][n0 + 64wn + 16j + 4(lane >> 4) + e]
+    const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ldc + n0 + 64 * wn + 4 * q;
+        u16x4 old[4];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = acc[i][j][e];
+                if (BETA) x += bf2f(old[j][e]);
+                o[e] = f2bf(x);
+            }
+            *reinterpret_cast<u16x4*>(crow_p + 16 * j) = o;
+        }
+    }
+}
+template __global__ void gemm_tn16_kernel<true>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
+                                                uint32_t, u16* __restrict__, int, int, int, int);
+template __global__ void gemm_tn16_kernel<false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
+                                                 uint32_t, u16* __restrict__, int, int, int, int);
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -409,6 +571,17 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
 #define SA_TN(BK, S, LW)                                                                      \
     if (beta) launch_tn<true, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);                \
     else launch_tn<false, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);
+    if (g_gemm_variant == 4) {
+        const int nwg = (int)((M / 256) * (N / 256));
+        const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+        if (beta)
+            hipLaunchKernelGGL((gemm_tn16_kernel<true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage, st, (const u16*)A,
+                               (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K);
+        else
+            hipLaunchKernelGGL((gemm_tn16_kernel<false>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage, st, (const u16*)A,
+                               (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K);
+        return;
+    }
     switch (g_gemm_variant) {
         case 1: SA_TN(32, 4, false) break;
         case 2: SA_TN(64, 2, true) break;

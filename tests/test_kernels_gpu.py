@@ -477,10 +477,20 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("variant", [2, 4])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
-def test_gemm_tn(M, N, K, accumulate):
-    """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands."""
+def test_gemm_tn(M, N, K, accumulate, variant):
+    """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands; pipeline
+    variants 2 (32x32x16 MFMA) and 4 (16x16x32 MFMA)."""
+    ext().gemm_set_variant(variant)
+    try:
+        _gemm_tn_case(M, N, K, accumulate)
+    finally:
+        ext().gemm_set_variant(2)
+
+
+def _gemm_tn_case(M, N, K, accumulate):
     torch.manual_seed(5)
     A_full = torch.randn(K, M + 64, device=DEV, dtype=torch.bfloat16)
     A = A_full[:, 64:]  # row stride M + 64, 128-B aligned start

@@ -1,0 +1,50 @@
+"""Per-step kernel time breakdown from a rocprofv3 rocpd database: steps are delimited by the optimizer's
+fused AdamW launches; reports the last complete step's kernels grouped by category (ms) and the GPU-busy
+vs wall span of that step.
+
+usage: python tools/rocpd_step.py <run_results.db>
+"""
+from __future__ import annotations
+
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def category(name: str) -> str:
+    rules = [("Cijk", "hipBLASLt GEMM"), ("gemm_tn", "wgrad GEMM (HIP)"), ("fa_fwd", "attention fwd"),
+             ("fa_bwd_dkdv", "attention bwd dK/dV"), ("fa_bwd_dq", "attention bwd dQ"), ("fa_bwd", "attention bwd other"),
+             ("adamw", "AdamW"), ("swiglu", "SwiGLU"), ("norm_", "norm"), ("colsum", "norm"), ("rope", "RoPE"),
+             ("xent", "cross-entropy"), ("embed", "embedding"), ("transpose_u16", "W^T transpose"),
+             ("sumsq", "grad norm"), ("cast_scale", "grad cast"), ("rccl", "RCCL"), ("nccl", "RCCL")]
+    for key, cat in rules:
+        if key in name:
+            return cat
+    return "other: " + re.sub(r"\(.*", "", name)[:60]
+
+
+def main() -> None:
+    c = sqlite3.connect(sys.argv[1])
+    rows = sorted(c.execute("select name, start, end from kernels"), key=lambda r: r[1])
+    adam = [i for i, r in enumerate(rows) if "adamw" in r[0]]
+    # step boundary = first kernel after a run of AdamW launches
+    ends = [i for j, i in enumerate(adam) if j + 1 == len(adam) or adam[j + 1] - i > 50]
+    if len(ends) < 2:
+        print("need two complete steps in the trace")
+        return
+    lo, hi = ends[-2] + 1, ends[-1] + 1
+    step = rows[lo:hi]
+    tot = defaultdict(float)
+    for name, s, e in step:
+        tot[category(name)] += (e - s) / 1e6
+    busy = sum(tot.values())
+    span = (step[-1][2] - step[0][1]) / 1e6
+    print(f"last complete step: {len(step)} kernels, busy {busy:.1f} ms, span {span:.1f} ms")
+    print("| category | ms | % of busy |\n|---|---|---|")
+    for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
+        print(f"| {k} | {v:.1f} | {100 * v / busy:.1f} |")
+
+
+if __name__ == "__main__":
+    main()
