@@ -307,7 +307,7 @@ uint32_t drop_threshold(double p) {
 }
 std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& cu_q,
                                const at::Tensor& cu_k, int64_t max_q, double scale, bool causal, int64_t window,
-                               double p_drop, int64_t seed, int64_t local_heads) {
+                               double p_drop, int64_t seed, int64_t local_heads, int64_t max_k) {
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v");
     TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type(), "flash_attn: q/k/v dtypes differ");
     TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "flash_attn: dropout probability must be in [0, 1)");
@@ -329,6 +329,22 @@ std::vector<at::Tensor> fa_fwd(const at::Tensor& q, const at::Tensor& k, const a
     a.local_heads = local_heads < 0 ? (int)H : (int)local_heads;
     a.scale_log2 = (float)(scale * 1.4426950408889634);
     a.p_drop = (float)p_drop; a.rp_drop = (float)(1.0 / (1.0 - p_drop)); a.seed = (uint32_t)seed; a.drop_thr = drop_threshold(p_drop);
+    const int64_t grp = H / k.size(1);
+    if (T > 0 && a.nseg > 0 && p_drop == 0.0 && max_q * grp <= 32) {
+        // short query segments (decode): GQA-packed rows, split-K over the keys, then a combine pass
+        DecArgs d{};
+        d.q = a.q; d.k = a.k; d.v = a.v;
+        d.q_tok = a.q_tok; d.q_head = a.q_head; d.k_tok = a.k_tok; d.k_head = a.k_head; d.v_tok = a.v_tok; d.v_head = a.v_head;
+        d.cu_q = a.cu_q; d.cu_k = a.cu_k; d.nseg = a.nseg; d.Hq = a.Hq; d.Hkv = a.Hkv; d.causal = a.causal;
+        d.window = a.window; d.local_heads = a.local_heads; d.scale_log2 = a.scale_log2; d.Tq = T;
+        sa_launch::fa_decode_plan(max_k > 0 ? max_k : k.size(0), a.Hkv, a.nseg, d.split_keys, d.nsplit);
+        auto part_o = at::empty({(int64_t)d.nsplit, T, H, D}, q.options().dtype(at::kFloat));
+        auto part_ml = at::empty({(int64_t)d.nsplit, T, H, 2}, q.options().dtype(at::kFloat));
+        d.part_o = part_o.data_ptr<float>(); d.part_ml = part_ml.data_ptr<float>();
+        d.o = a.o; d.o_tok = a.o_tok; d.o_head = a.o_head; d.lse = a.lse; d.lse_stride = a.lse_stride;
+        sa_launch::fa_decode(d, (int)D, q.scalar_type() == at::kHalf, cur_stream());
+        return {o, lse};
+    }
     if (T > 0 && a.nseg > 0) sa_launch::fa_fwd(a, (int)D, (int)max_q, q.scalar_type() == at::kHalf, cur_stream());
     return {o, lse};
 }
@@ -492,6 +508,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
-    m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);
+    m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("max_k") = -1);
     m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);
 }

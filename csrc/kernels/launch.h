@@ -73,6 +73,25 @@ namespace sa_launch {
 void fa_fwd(const FwdArgs& a, int D, int max_q, bool f16, hipStream_t st);
 }
 
+// flash-decoding (short query segments, GQA rows packed into one wave, split-K + combine)
+struct DecArgs {
+    const uint16_t* q; const uint16_t* k; const uint16_t* v;
+    int64_t q_tok, q_head, k_tok, k_head, v_tok, v_head;
+    const int* cu_q; const int* cu_k;
+    int nseg, Hq, Hkv, causal, window, local_heads;
+    float scale_log2;
+    int split_keys, nsplit;
+    int64_t Tq;
+    float* part_o;   // [nsplit][Tq][Hq][D]
+    float* part_ml;  // [nsplit][Tq][Hq][2] running max (log2 units) and sum
+    uint16_t* o; int64_t o_tok, o_head;
+    float* lse; int64_t lse_stride;
+};
+namespace sa_launch {
+void fa_decode_plan(int64_t max_k, int Hkv, int nseg, int& split_keys, int& nsplit);
+void fa_decode(const DecArgs& a, int D, bool f16, hipStream_t st);
+}
+
 struct BwdArgs {
     const uint16_t* q; const uint16_t* k; const uint16_t* v; const uint16_t* dO;
     const float* lse; float* delta; float* lse2;

@@ -115,7 +115,7 @@ class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window, p_drop=0.0, seed=0,  # type: ignore[override]
                 local_heads=-1):
-        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads)
+        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
         ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
         ctx.cfg = (max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
@@ -151,7 +151,7 @@ class _RopeFlashAttn(torch.autograd.Function):
         qi, ki, vi = (_view(base, sp) for sp in specs)
         q = ext().rope(qi, cos, sin, pos, rot_dim, seq_len, interleaved, False)
         k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
-        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads)
+        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
         ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
         ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o

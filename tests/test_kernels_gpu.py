@@ -610,3 +610,51 @@ def test_linear_dgrad_with_transposed_weight_cache():
     mg.multi_linear(x, w).backward(g)
     ref2 = g.float() @ torch.cat(w, 0).detach().float()
     torch.testing.assert_close(x.grad.float(), ref2, atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("Lq,Lks,Hq,Hk,D,causal,window,local_heads,dtype", [
+    (1, [4096], 32, 8, 128, True, -1, None, torch.bfloat16),       # 7B cached decode step
+    (1, [17, 1000, 3], 8, 8, 64, True, -1, None, torch.bfloat16),  # MHA, ragged caches, one segment per sequence
+    (4, [333, 64], 16, 2, 128, True, -1, None, torch.float16),    # 4-token chunk x 8 q heads = 32 packed rows
+    (2, [700], 8, 2, 128, True, 50, 3, torch.bfloat16),           # mixed local/global heads
+    (3, [130, 90], 4, 4, 32, False, -1, None, torch.bfloat16),    # non-causal, D 32
+])
+def test_flash_decoding(Lq, Lks, Hq, Hk, D, causal, window, local_heads, dtype):
+    """Short query segments take the split-K flash-decoding kernels (GQA rows packed, combine pass); output and
+    lse against the fp32 reference."""
+    torch.manual_seed(0)
+    n = len(Lks)
+    cu_q = torch.arange(0, (n + 1) * Lq, Lq, device=DEV, dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(Lks).cumsum(0)), device=DEV, dtype=torch.int32)
+    q = torch.randn(n * Lq, Hq, D, device=DEV, dtype=dtype)
+    k = torch.randn(sum(Lks), Hk, D, device=DEV, dtype=dtype)
+    v = torch.randn(sum(Lks), Hk, D, device=DEV, dtype=dtype)
+    scale = 1 / math.sqrt(D)
+    with torch.no_grad():
+        o = attention.flash_attention(q, k, v, cu_q, cu_k, Lq, max(Lks), scale, causal, None if window < 0 else window,
+                                      local_heads=local_heads)
+        o2, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, Lq, scale, causal, window, 0.0, 0,
+                               -1 if local_heads is None else local_heads, max(Lks))
+    ref = attention.attention_reference(q.float(), k.float(), v.float(), cu_q, cu_k, scale, causal, window,
+                                        local_heads=local_heads)
+    torch.testing.assert_close(o.float(), ref, atol=2e-2, rtol=2e-2)
+    assert torch.equal(o, o2)
+    # lse of the first segment's rows against log-sum-exp of the reference scores
+    qq, kk = q[:Lq].float(), k[: Lks[0]].float().repeat_interleave(Hq // Hk, 1)
+    s = torch.einsum("qhd,khd->hqk", qq, kk) * scale
+    qpos = torch.arange(Lq, device=DEV)[:, None] + Lks[0] - Lq
+    kpos = torch.arange(Lks[0], device=DEV)[None, :]
+    ok = torch.ones(Lq, Lks[0], dtype=torch.bool, device=DEV)
+    if causal:
+        ok &= kpos <= qpos
+    okw = ok & (kpos >= qpos - window) & ((kpos <= qpos + window) if not causal else ok) if window >= 0 else ok
+    nl = Hq if local_heads is None else local_heads
+    mask = torch.stack([okw if h < nl else ok for h in range(Hq)])
+    lse_ref = torch.logsumexp(s.masked_fill(~mask, float("-inf")), -1)
+    torch.testing.assert_close(lse[:, :Lq], lse_ref, atol=2e-2, rtol=1e-3)
+
+
+def test_flash_decoding_forward_with_prefill_backward():
+    """Tiny training segments (max_q x group <= 32) run the decode forward and the regular backward kernels."""
+    _attn_case([7, 5], 4, 1, 64, True)
+    _attn_case([8], 4, 4, 128, False)
