@@ -25,6 +25,14 @@ after the dgrad GEMM, runs the weight-gradient GEMM while RCCL moves ``dX`` over
 before returning (Megatron's async TP all-reduce; the reference runs them back to back,
 ``column_parallel_linear.py:137-139``).
 
+Weight-gradient GEMMs are off the backward's critical path (only the optimizer consumes them), so the
+GEMM-fused ones run on a side HIP stream (``SCALING_AMD_WGRAD_STREAM=0`` disables): the next dgrad /
+attention / norm kernels of the backward are enqueued without waiting for them, and the hardware fills the
+CUs a wgrad grid leaves idle in its last wave with the other stream's workgroups.  Ordering: the side stream
+waits for the main stream before each wgrad; the optimizer's bucket reductions wait for the side stream;
+an autograd final callback makes the main stream wait for it at the end of every backward, so ``.grad`` is
+stream-ordered for any reader after ``backward()`` exactly as without the side stream.
+
 Input gradient ``dX = dY W``: hipBLASLt runs that NN layout at ~1.3 PF/s on gfx950 but the forward's
 ``X W^T`` layout at ~1.6 PF/s.  With a transposed copy ``W^T`` the backward is ``dY (W^T)^T`` — the forward
 layout — so training keeps a transposed copy of every weight (LDS-tiled transpose kernel, ~12 GB for the 7B
@@ -44,6 +52,44 @@ from ....ops.gemm import transpose2d, wgrad
 
 _GEN = [0]
 _WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
+
+
+_WGRAD_STREAM_ENABLED = os.environ.get("SCALING_AMD_WGRAD_STREAM", "1") != "0"
+_wgrad_streams: dict[int, Any] = {}
+_sync_queued = [False]
+
+
+def wgrad_stream(device: torch.device) -> Optional[Any]:
+    """The side stream of this device's GEMM-fused weight-gradient GEMMs (None when disabled / not on a GPU)."""
+    if not _WGRAD_STREAM_ENABLED or device.type != "cuda":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _wgrad_streams.get(idx)
+    if st is None:
+        st = torch.cuda.Stream(device=idx)
+        _wgrad_streams[idx] = st
+    return st
+
+
+def sync_wgrad_stream(device: torch.device) -> None:
+    """Makes the current stream wait for every weight-gradient GEMM issued so far on ``device``."""
+    if device.type != "cuda":
+        return
+    st = _wgrad_streams.get(device.index if device.index is not None else torch.cuda.current_device())
+    if st is not None:
+        torch.cuda.current_stream(device).wait_stream(st)
+
+
+def _queue_end_of_backward_sync(device: torch.device) -> None:
+    if _sync_queued[0]:
+        return
+    _sync_queued[0] = True
+
+    def _sync() -> None:
+        _sync_queued[0] = False
+        sync_wgrad_stream(device)
+
+    torch.autograd.Variable._execution_engine.queue_callback(_sync)
 
 
 def invalidate_transposed_weights() -> None:
@@ -138,7 +184,16 @@ class _MultiLinear(torch.autograd.Function):
                 g2 = g2 * col
             target = _main_grad_target(weights)
             if target is not None:
-                wgrad(g2, x2, target, accumulate=True)
+                ws = wgrad_stream(g2.device)
+                if ws is not None:
+                    ws.wait_stream(torch.cuda.current_stream(g2.device))
+                    with torch.cuda.stream(ws):
+                        wgrad(g2, x2, target, accumulate=True)
+                    g2.record_stream(ws)  # keep the operands' memory until the side stream is done
+                    x2.record_stream(ws)
+                    _queue_end_of_backward_sync(g2.device)
+                else:
+                    wgrad(g2, x2, target, accumulate=True)
                 for wt in weights:
                     cb = getattr(wt, "_sa_grad_ready", None)
                     if cb is not None:

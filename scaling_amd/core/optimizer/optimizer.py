@@ -32,7 +32,7 @@ import torch.distributed as dist
 
 from ...ops import optim as optim_ops
 from ..logging import logger
-from ..nn.linear.main_grad import invalidate_transposed_weights
+from ..nn.linear.main_grad import invalidate_transposed_weights, sync_wgrad_stream, wgrad_stream
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
 from ..utils.safe_load import safe_load
@@ -149,9 +149,13 @@ class Optimizer(BaseOptimizer):
 
         if self._comm_stream is not None:
             self._comm_stream.wait_stream(torch.cuda.current_stream(self.topology.device))
+            ws = wgrad_stream(self.topology.device)  # GEMM-accumulated grads land on the wgrad side stream
+            if ws is not None:
+                self._comm_stream.wait_stream(ws)
             with torch.cuda.stream(self._comm_stream):
                 run()
         else:
+            sync_wgrad_stream(self.topology.device)
             run()
 
     def prepare_grad_sync(self) -> None:
@@ -259,6 +263,7 @@ class Optimizer(BaseOptimizer):
 
     def step(self) -> OptimizerStepOutput:
         self.wait_param_sync()  # parameters never touched by a forward (frozen / unused) still must land
+        sync_wgrad_stream(self.topology.device)  # (also done at the end of every backward)
         self.step_index += 1
         for g in self.parameter_groups:
             g.set_dummy_grad()
