@@ -26,7 +26,8 @@ before returning (Megatron's async TP all-reduce; the reference runs them back t
 ``column_parallel_linear.py:137-139``).
 
 Weight-gradient GEMMs are off the backward's critical path (only the optimizer consumes them), so the
-GEMM-fused ones run on a side HIP stream (``SCALING_AMD_WGRAD_STREAM=0`` disables): the next dgrad /
+GEMM-fused ones can run on a side HIP stream (``SCALING_AMD_WGRAD_STREAM=1``; off by default: measured 2 %
+slower on the 7B step, profiles/bench_7b_r2_wgrad_stream_ab.log — concurrent MFMA grids thrash L2/LDS): the next dgrad /
 attention / norm kernels of the backward are enqueued without waiting for them, and the hardware fills the
 CUs a wgrad grid leaves idle in its last wave with the other stream's workgroups.  Ordering: the side stream
 waits for the main stream before each wgrad; the optimizer's bucket reductions wait for the side stream;
@@ -54,7 +55,7 @@ _GEN = [0]
 _WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
 
 
-_WGRAD_STREAM_ENABLED = os.environ.get("SCALING_AMD_WGRAD_STREAM", "1") != "0"
+_WGRAD_STREAM_ENABLED = os.environ.get("SCALING_AMD_WGRAD_STREAM", "0") == "1"
 _wgrad_streams: dict[int, Any] = {}
 _sync_queued = [False]
 
