@@ -6,7 +6,7 @@ cd "$R"
 mkdir -p gpurun_out
 TAG=${TAG:-run}
 for rep in 1 2; do
-  for cfg in ${CFGS:-"2 4" "4 2"}; do
+  for cfg in "2 4" "4 2"; do
     set -- $cfg
     timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --micro-batch $1 --grad-acc $2 \
         > gpurun_out/bench_${TAG}_mb$1_acc$2_$rep.log 2>&1
