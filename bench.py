@@ -45,8 +45,10 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--model", type=str, default="llama2_7b")
     p.add_argument("--seq-len", type=int, default=4096)
-    p.add_argument("--micro-batch", type=int, default=2)
-    p.add_argument("--grad-acc", type=int, default=4)
+    # 8 sequences of 4096 tokens per GPU per step; 4 x 2 measured +2.8 % over 2 x 4 (bigger GEMMs, fewer
+    # weight-gradient read-modify-writes; profiles/bench_7b_r2_microbatch_ab.log)
+    p.add_argument("--micro-batch", type=int, default=4)
+    p.add_argument("--grad-acc", type=int, default=2)
     p.add_argument("--tp", type=int, default=1)
     p.add_argument("--pp", type=int, default=1)
     p.add_argument("--activation-checkpointing", type=str, default="disabled",
@@ -325,6 +327,7 @@ def _worker(a: argparse.Namespace) -> None:
                 "world_size_seen": dist.get_world_size(),
                 "per_rank_ms_per_step": [round(1000.0 * float(t) / a.steps, 2) for t in times.tolist()],
                 "dp_param_checksum_agree": dp_agree,
+                "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
             },
         }
         if a.profile_json:
