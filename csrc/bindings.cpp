@@ -281,8 +281,18 @@ bool gemm_tn_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
 void gemm_tn(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool accumulate) {
     TORCH_CHECK(gemm_tn_ok(A, B, C), "gemm_tn: unsupported operands (bf16 2-D, M/N multiple of 256, K of 64)");
     const at::DeviceGuard g(A.device());
+    static int slots = -1;  // one 256x256 tile per CU
+    if (slots < 0) {
+        hipDeviceProp_t prop;
+        slots = hipGetDeviceProperties(&prop, A.device().index()) == hipSuccess ? prop.multiProcessorCount : 0;
+    }
+    int full_blocks = -1, split = 1;
+    const int64_t ws_floats = sa_launch::gemm_tn_plan(A.size(1), B.size(1), A.size(0), slots, full_blocks, split);
+    at::Tensor ws;
+    if (ws_floats > 0) ws = at::empty({ws_floats}, A.options().dtype(at::kFloat));
     sa_launch::gemm_tn(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), A.size(1),
-                       B.size(1), A.size(0), accumulate, cur_stream());
+                       B.size(1), A.size(0), accumulate, cur_stream(), full_blocks, split,
+                       ws_floats > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
 at::Tensor gemm_tn_timing(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {

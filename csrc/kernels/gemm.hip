@@ -16,6 +16,8 @@
 //  * Grid: XCD-aware bijective remap, then 8-row groups of tiles so the 32 tiles resident on one XCD
 //    cover an 8x4 block and share A/B panels in its L2.
 //  * Epilogue: C = acc (+ C) with one bf16 rounding (beta = 1 accumulates into a main-grad buffer).
+#include <algorithm>
+
 #include "common.h"
 #include "flash_attn.h"
 #include "launch.h"
@@ -140,7 +142,8 @@ template <bool BETA, int BK, int STAGES, bool LATEWAIT, bool TIMING = false>
 __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
                                                          const u16* __restrict__ B, int ldb, uint32_t b_bytes,
                                                          u16* __restrict__ C, int ldc, int M, int N, int K,
-                                                         uint64_t* __restrict__ dbg = nullptr) {
+                                                         uint64_t* __restrict__ dbg, int full_blocks, int tail_split,
+                                                         float* __restrict__ ws) {
     using G = Cfg<BK>;
     constexpr int KS = BK / 16;                   // MFMA k-steps per K-tile
     constexpr bool SPLIT = STAGES == 2;           // group 0 stages A images, group 1 stages B images
@@ -153,9 +156,19 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave >> 2, wn = wave & 3;  // wm doubles as the ping-pong group
 
-    // tile coordinates
-    const int tm = M / 256, tn = N / 256, nwg = tm * tn;
-    const int v = xcd_remap(blockIdx.x, nwg);
+    // tile coordinates.  Blocks [0, full_blocks) own whole tiles (XCD remap over them); with a split tail the
+    // remaining tiles [full_blocks, nwg) run as tail_split K-slices each (one block per slice, the grid's last
+    // round) writing fp32 partials that gemm_tn_combine adds into C — the last round is full instead of ragged.
+    const int tm = M / 256, tn = N / 256;
+    int v, k_lo = 0, nk = K / BK, unit = -1;
+    if ((int)blockIdx.x < full_blocks) {
+        v = xcd_remap(blockIdx.x, full_blocks);
+    } else {
+        unit = (int)blockIdx.x - full_blocks;
+        v = full_blocks + unit / tail_split;
+        nk /= tail_split;
+        k_lo = (unit % tail_split) * nk;
+    }
     const int group = kGroupM * tn;
     const int first_m = (v / group) * kGroupM;
     const int gm = min(tm - first_m, kGroupM);
@@ -176,11 +189,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nk = K / BK;
 #define SA_ISSUE(t_)                                                                                      \
     if (stager) {                                                                                         \
         char* st_ = smem + ((t_) % STAGES) * G::kStage;                                                   \
-        const int k0_ = (t_) * BK;                                                                        \
+        const int k0_ = (k_lo + (t_)) * BK;                                                                        \
         da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave);          \
         db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave); \
     }
@@ -201,7 +213,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
 #define SA_ISSUE_G(t_)                                                                                    \
         {                                                                                                 \
             char* st_ = smem + ((t_) & 1) * G::kStage;                                                    \
-            const int k0_ = (t_) * BK;                                                                    \
+            const int k0_ = (k_lo + (t_)) * BK;                                                                    \
             if (wm == 0) da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave); \
             else db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave); \
         }
@@ -243,7 +255,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
             // group 1 threads its B-image pieces for tile t+2 between the MFMAs (one per 32 / NP MFMAs) so
             // they issue in the matrix pipe's shadow
             const bool stage_b = wm == 1 && t + 2 < nk;
-            const int soff_b = __builtin_amdgcn_readfirstlane(((t + 2) * BK * ldb + n0) * 2);
+            const int soff_b = __builtin_amdgcn_readfirstlane(((k_lo + t + 2) * BK * ldb + n0) * 2);
             char* st_b = smem + (t & 1) * G::kStage + G::kImg;
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
@@ -327,6 +339,23 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
 
     // epilogue: acc[i][j][4q + e] = C[m0 + 128wm + 32i + (lane & 31)][n0 + 64wn + 32j + 8q + 4h + e]
     const int h = lane >> 5, c = lane & 31;
+    if (unit >= 0) {  // K-slice of a tail tile: fp32 partial [256][256] at ws + unit * 65536
+        float* wp = ws + (int64_t)unit * 65536;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float* rp = wp + (128 * wm + 32 * i + c) * 256 + 64 * wn + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f32x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(rp + 32 * j + 8 * q) = o;
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         u16* crow_p = C + (int64_t)(m0 + 128 * wm + 32 * i + c) * ldc + n0 + 64 * wn + 4 * h;
@@ -521,21 +550,51 @@ template __global__ void gemm_tn16_kernel<false>(const u16* __restrict__, int, u
     template __global__ void gemm_tn_kernel<BETA, BK, S, LW, TM>(const u16* __restrict__, int, uint32_t,            \
                                                                  const u16* __restrict__, int, uint32_t,            \
                                                                  u16* __restrict__, int, int, int, int,             \
-                                                                 uint64_t* __restrict__);
+                                                                 uint64_t* __restrict__, int, int, float* __restrict__);
 #define SA_GEMM_INST2(BK, S, LW) SA_GEMM_INST(true, BK, S, LW, false) SA_GEMM_INST(false, BK, S, LW, false)
 SA_GEMM_INST2(32, 4, false) SA_GEMM_INST2(32, 4, true) SA_GEMM_INST2(64, 2, true) SA_GEMM_INST2(32, 5, true)
 SA_GEMM_INST(false, 32, 4, true, true) SA_GEMM_INST(false, 64, 2, true, true)
 #undef SA_GEMM_INST2
 #undef SA_GEMM_INST
 
+// tail tile v (>= full_blocks): C[m0 + r][n0 + c] = (beta ? C : 0) + sum of its K-slice partials; block (tile, 4 rows)
+__global__ __launch_bounds__(256) void gemm_tn_combine_kernel(const float* __restrict__ ws, u16* __restrict__ C, int ldc,
+                                                              int M, int N, int full_blocks, int split, int beta) {
+    const int tm = M / 256, tn = N / 256;
+    const int v = full_blocks + (int)blockIdx.x;
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+    const int row = 4 * (int)blockIdx.y + (threadIdx.x >> 6), col = (threadIdx.x & 63) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wp = ws + (int64_t)blockIdx.x * split * 65536 + row * 256 + col;
+    for (int p = 0; p < split; ++p) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(wp + (int64_t)p * 65536);
+        acc += x;
+    }
+    u16* cp = C + (int64_t)(m0 + row) * ldc + n0 + col;
+    u16x4 o;
+    const u16x4 old = beta ? *reinterpret_cast<const u16x4*>(cp) : u16x4{0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[e] + (beta ? bf2f(old[e]) : 0.f));
+    *reinterpret_cast<u16x4*>(cp) = o;
+}
+
 template <bool BETA, int BK, int STAGES, bool LW>
 void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-               int64_t K, hipStream_t st) {
+               int64_t K, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr) {
     const int nwg = (int)((M / 256) * (N / 256));
+    if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
+    const int grid = full_blocks + (nwg - full_blocks) * split;
     const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
-    hipLaunchKernelGGL((gemm_tn_kernel<BETA, BK, STAGES, LW>), dim3(nwg), dim3(512), STAGES * Cfg<BK>::kStage, st,
+    hipLaunchKernelGGL((gemm_tn_kernel<BETA, BK, STAGES, LW>), dim3(grid), dim3(512), STAGES * Cfg<BK>::kStage, st,
                        (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
-                       (int)K, nullptr);
+                       (int)K, nullptr, full_blocks, split, ws);
+    if (split > 1)
+        hipLaunchKernelGGL(gemm_tn_combine_kernel, dim3(nwg - full_blocks, 64), dim3(256), 0, st, (const float*)ws, (u16*)C,
+                           (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
 }
 
 }  // namespace sa_gemm
@@ -555,19 +614,42 @@ void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (g_gemm_variant == 2)
         hipLaunchKernelGGL((gemm_tn_kernel<false, 64, 2, true, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra,
                            st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M,
-                           (int)N, (int)K, dbg);
+                           (int)N, (int)K, dbg, nwg, 1, nullptr);
     else
         hipLaunchKernelGGL((gemm_tn_kernel<false, 32, 4, true, true>), dim3(nwg), dim3(512), 4 * Cfg<32>::kStage + extra,
                            st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M,
-                           (int)N, (int)K, dbg);
+                           (int)N, (int)K, dbg, nwg, 1, nullptr);
 }
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
     return M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 &&
            ldb % 8 == 0 && ldc % 4 == 0 && K * lda * 2 < (int64_t(1) << 31) && K * ldb * 2 < (int64_t(1) << 31) &&
            ldc < (1 << 30);
 }
+// Split plan for the ragged last round: with nwg tiles on `slots` workgroup slots (one 256x256 tile per CU), the
+// r = nwg % slots tiles of the last round leave slots - r CUs idle; when r <= slots / 2 those tiles run as
+// `split` K-slices each (<= 4, >= 4 K-tiles per slice) and a combine pass adds the fp32 partials into C.
+// Variant 2 only.  Returns the fp32 workspace floats needed (0: no split).
+int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_blocks, int& split) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    full_blocks = nwg;
+    split = 1;
+    if (g_gemm_variant != 2 || slots <= 0) return 0;
+    const int r = nwg % slots, nk = (int)(K / 64);
+    if (r == 0 || 2 * r > slots) return 0;
+    int s = std::min(slots / r, 4);
+    while (s > 1 && (nk % s != 0 || nk / s < 4)) --s;
+    if (s <= 1) return 0;
+    split = s;
+    full_blocks = nwg - r;
+    return (int64_t)r * s * 65536;
+}
 void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-             int64_t K, bool beta, hipStream_t st) {
+             int64_t K, bool beta, hipStream_t st, int full_blocks, int split, float* ws) {
+    if (g_gemm_variant == 2 && split > 1) {
+        if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        return;
+    }
 #define SA_TN(BK, S, LW)                                                                      \
     if (beta) launch_tn<true, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);                \
     else launch_tn<false, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);

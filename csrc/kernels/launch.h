@@ -53,8 +53,9 @@ void gemm_set_variant(int v);
 void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                     int64_t K, uint64_t* dbg, hipStream_t st);
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_blocks, int& split);
 void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-             int64_t K, bool beta, hipStream_t st);
+             int64_t K, bool beta, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr);
 }  // namespace sa_launch
 
 // flash attention (bf16, head dim 32/64/128)

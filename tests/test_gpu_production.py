@@ -59,9 +59,11 @@ def test_flash_attention_7b_shape():
 
 
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad_gemm_7b_mlp_shape(accumulate):
+@pytest.mark.parametrize("T,N,K", [(8192, 11008, 4096), (16384, 6144, 4096), (16384, 22016, 4096)])
+def test_wgrad_gemm_7b_shapes(accumulate, T, N, K):
+    """MLP-out, QKV and gate/up weight gradients at 8k / 16k tokens; the last two have a ragged last round
+    of 256x256 tiles that runs as split-K slices plus a combine pass."""
     torch.manual_seed(0)
-    T, N, K = 8192, 11008, 4096
     dy = torch.randn(T, N, device=DEV, dtype=torch.bfloat16)
     x = torch.randn(T, K, device=DEV, dtype=torch.bfloat16)
     out = (0.5 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)

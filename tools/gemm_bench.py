@@ -30,7 +30,7 @@ def timeit(fn, iters):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tokens", type=int, default=8192)
+    ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", type=str, default="", help="comma list of gemm_tn pipeline variants to compare")
     a = ap.parse_args()
