@@ -626,8 +626,9 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
            ldc < (1 << 30);
 }
 // Split plan for the ragged last round: with nwg tiles on `slots` workgroup slots (one 256x256 tile per CU), the
-// r = nwg % slots tiles of the last round leave slots - r CUs idle; when r <= slots / 2 those tiles run as
-// `split` K-slices each (<= 4, >= 4 K-tiles per slice) and a combine pass adds the fp32 partials into C.
+// r = nwg % slots tiles of the last round leave slots - r CUs idle; those tiles run as `split` K-slices each
+// (2..4, >= 4 K-tiles per slice, chosen to minimise the tail's rounds x slice length) and a combine pass adds the
+// fp32 partials into C.
 // Variant 2 only.  Returns the fp32 workspace floats needed (0: no split).
 int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_blocks, int& split) {
     const int nwg = (int)((M / 256) * (N / 256));
@@ -635,10 +636,16 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     split = 1;
     if (g_gemm_variant != 2 || slots <= 0) return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
-    if (r == 0 || 2 * r > slots) return 0;
-    int s = std::min(slots / r, 4);
-    while (s > 1 && (nk % s != 0 || nk / s < 4)) --s;
-    if (s <= 1) return 0;
+    if (r == 0) return 0;
+    // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
+    int s = 1;
+    double best = 1.0;
+    for (int c = 2; c <= 4; ++c) {
+        if (nk % c != 0 || nk / c < 4) continue;
+        const double cost = (double)((r * c + slots - 1) / slots) / c;
+        if (cost < best - 1e-9) { best = cost; s = c; }
+    }
+    if (s <= 1 || best > 0.8) return 0;
     split = s;
     full_blocks = nwg - r;
     return (int64_t)r * s * 65536;
