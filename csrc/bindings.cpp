@@ -5,6 +5,9 @@
 #include <c10/core/DeviceGuard.h>
 
 #include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
 #include "kernels/launch.h"
 
 namespace {
@@ -248,6 +251,48 @@ void cast_scale_(const at::Tensor& x, at::Tensor y, double scale) {
     TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "cast_scale: bad args");
     const at::DeviceGuard g(x.device());
     sa_launch::cast_scale(dt(x), dt(y), x.data_ptr(), y.data_ptr(), x.numel(), (float)scale, cur_stream());
+}
+
+// ------------------------------------------------------------------ one-shot all-reduce (IPC peer buffers)
+// registered buffer: [slot 0 | slot 1 | flag row]; returns (device address, IPC handle bytes)
+py::tuple ar_alloc(int64_t nbytes, int64_t device) {
+    TORCH_CHECK(nbytes > 0, "ar_alloc: size");
+    TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "ar_alloc: hipSetDevice");
+    void* p = nullptr;
+    TORCH_CHECK(hipMalloc(&p, (size_t)nbytes) == hipSuccess, "ar_alloc: hipMalloc failed");
+    TORCH_CHECK(hipMemset(p, 0, (size_t)nbytes) == hipSuccess, "ar_alloc: hipMemset failed");
+    hipIpcMemHandle_t h;
+    TORCH_CHECK(hipIpcGetMemHandle(&h, p) == hipSuccess, "ar_alloc: hipIpcGetMemHandle failed");
+    return py::make_tuple((int64_t)reinterpret_cast<uintptr_t>(p), py::bytes(reinterpret_cast<const char*>(&h), sizeof(h)));
+}
+int64_t ar_open(const std::string& handle, int64_t device) {
+    TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "ar_open: bad handle size");
+    TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "ar_open: hipSetDevice");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle.data(), sizeof(h));
+    void* p = nullptr;
+    TORCH_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess, "ar_open: hipIpcOpenMemHandle failed");
+    return (int64_t)reinterpret_cast<uintptr_t>(p);
+}
+void ar_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>((uintptr_t)ptr)); }
+void ar_free(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>((uintptr_t)ptr)); }
+// x (+)= sum over ranks, in place; x is first copied into this rank's slot `slot_off`
+void ar_allreduce(at::Tensor x, const std::vector<int64_t>& bases, int64_t rank, int64_t slot_off, int64_t flag_off,
+                  int64_t epoch, bool signal, at::Tensor err) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.is_contiguous(), "ar_allreduce: contiguous input");
+    TORCH_CHECK(bases.size() >= 1 && bases.size() <= 8 && rank >= 0 && rank < (int64_t)bases.size(), "ar_allreduce: ranks");
+    const int vec = x.scalar_type() == at::kFloat ? 4 : 8;
+    TORCH_CHECK(x.numel() % vec == 0, "ar_allreduce: numel must be a multiple of the vector width");
+    TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt, "ar_allreduce: err must be a cuda int32 tensor");
+    const at::DeviceGuard g(x.device());
+    char* own = reinterpret_cast<char*>((uintptr_t)bases[rank]) + slot_off;
+    TORCH_CHECK(hipMemcpyAsync(own, x.data_ptr(), x.nbytes(), hipMemcpyDeviceToDevice, cur_stream()) == hipSuccess,
+                "ar_allreduce: slot copy");
+    std::vector<char*> b(bases.size());
+    for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>((uintptr_t)bases[i]);
+    sa_launch::oneshot_allreduce(dt(x), b.data(), (int)bases.size(), (int)rank, slot_off, flag_off, (uint32_t)epoch,
+                                 signal, x.data_ptr(), x.numel(), err.data_ptr<int>(), cur_stream());
 }
 
 // ------------------------------------------------------------------ transpose (dgrad weight cache)
@@ -501,6 +546,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
     m.def("gemm_set_variant", &sa_launch::gemm_set_variant, "select the gemm_tn pipeline variant (benchmarking)");
     m.def("gemm_tn_timing", &gemm_tn_timing, "profiling: per-phase s_memtime stamps of gemm_tn workgroup 0");
+    m.def("ar_alloc", &ar_alloc, "one-shot all-reduce: allocate + IPC-export a registered buffer");
+    m.def("ar_open", &ar_open, "one-shot all-reduce: map a peer's registered buffer");
+    m.def("ar_close", &ar_close, "unmap a peer buffer");
+    m.def("ar_free", &ar_free, "free an own registered buffer");
+    m.def("ar_allreduce", &ar_allreduce, "one-shot all-reduce of x over the registered buffers (in place)");
     m.def("transpose_ok", &transpose_ok, "whether transpose2d supports this tensor");
     m.def("transpose2d", &transpose2d, "x^T (contiguous) for 2-byte 2-D matrices");
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");

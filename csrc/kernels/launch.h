@@ -127,3 +127,9 @@ void act_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t n, int 
 void dropout(int dtype, const void* x, const void* res, void* out, int64_t n, uint32_t seed, uint32_t thr, float rp,
              hipStream_t st);
 }  // namespace sa_launch
+
+namespace sa_launch {
+// one-shot all-reduce over IPC-mapped peer buffers (oneshot_allreduce.hip)
+void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64_t slot_off, int64_t flag_off,
+                       uint32_t epoch, bool signal, void* out, int64_t n, int* err, hipStream_t st);
+}

@@ -38,6 +38,12 @@ def raw_all_reduce(x: torch.Tensor, size: int, group: Any) -> torch.Tensor:
     if size == 1:
         return x
     x = x.contiguous()
+    if x.is_cuda:
+        from .custom_allreduce import for_group
+
+        ar = for_group(group, x.device)  # opt-in one-shot xGMI all-reduce for small messages
+        if ar is not None and ar(x):
+            return x
     dist.all_reduce(x, group=group)
     return x
 
