@@ -89,6 +89,10 @@ struct Stage {
 };
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// Placed at the top of a rarely taken, wave-uniform block (boundary-tile mask, lazy rescale): an empty volatile asm
+// cannot be speculated, so the optimiser keeps the block behind its scalar branch instead of if-converting it into
+// per-element compares + selects that every tile would execute.
+__device__ __forceinline__ void mask_fence() { asm volatile(""); }
 
 // dword 3 of a raw buffer resource on gfx9/CDNA (32-bit data format, no swizzle); out-of-range
 // loads return 0

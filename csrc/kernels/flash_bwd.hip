@@ -292,8 +292,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
     const int win = hq < a.local_heads ? a.window : -1;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+              lq = lane & 31;
+    const int wave_u = wave;  // wave-uniform: qw0 and the mask test below are scalar
     const int off = Lk - Lq;
     const int qwg0 = qt * 128, qw0 = qwg0 + wave * 32, myq = qw0 + lq;
     const int qlast = min(qwg0 + 127, Lq - 1);
@@ -351,18 +352,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
                 dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row(ks)), df[ks], dp);
             }
             // key of register j: kt + 32b + 4h + crow(j)
-            int hi = 1 << 30, low = -1 << 30;
-            if (need_mask) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = fast_exp2(__builtin_fmaf(s[r], c2, nl2));
+            if (need_mask) {  // boundary tiles only: a real (wave-uniform) branch, not per-element selects
+                mask_fence();
                 const int base = kt + 32 * b + 4 * h;
-                hi = Lk - 1 - base;
+                int hi = Lk - 1 - base, low = -1 << 30;
                 if (a.causal) hi = min(hi, myq + off - base);
                 else if (win >= 0) hi = min(hi, myq + off + win - base);
                 if (win >= 0) low = myq + off - win - base;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[r] = (crow(r) <= hi && crow(r) >= low) ? s[r] : 0.f;
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                float p = fast_exp2(__builtin_fmaf(s[r], c2, nl2));
-                if (need_mask) p = (crow(r) <= hi && crow(r) >= low) ? p : 0.f;
+                const float p = s[r];
                 if constexpr (DROP) {
                     const bool keep = drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(r), a.drop_thr);
                     dp[r] = p * ((keep ? dp[r] * a.rp_drop : 0.f) - dlt);

@@ -202,7 +202,10 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
     const int win = hq < a.local_heads ? a.window : -1;  // per-head window (mixed local/global heads)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, lq = lane & 31;
+    // wave index through readfirstlane: everything derived from it (qw0, the mask test) is provably
+    // wave-uniform, so the boundary-tile mask is a real branch instead of per-element selects
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
+              lq = lane & 31;
     const int off = Lk - Lq;
     const int qwg0 = qt * C::BM, qw0 = qwg0 + 32 * wave, myq = qw0 + lq;
     const int qlast = min(qwg0 + C::BM - 1, Lq - 1);
@@ -273,6 +276,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
                                (win >= 0 && (kt < qw0 + 31 + off - win ||
                                                   (!a.causal && kt + C::KT - 1 > qw0 + off + win)));
         if (need_mask) {
+            mask_fence();
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
                 const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
@@ -293,6 +297,7 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
         mx = vmax3(mx, s[1][15], s[1][15]);
         const float mrow = max_xchg32(mx) * c2;
         if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {  // rare after the first tiles
+            mask_fence();
             const float mnew = fmaxf(m, mrow);
             const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
             l *= alpha;

@@ -53,19 +53,20 @@ struct Cfg {
     static constexpr int kPieces = kImg / 1024 / kWaves;  // LDS-DMA instructions per wave per image
 };
 
-// this wave's LDS-DMA pieces of one [BK][256] operand image: per-lane byte offsets relative to the K-tile's
-// first element (source-permuted swizzle), issued with the tile offset as the scalar soffset
+// this wave's LDS-DMA pieces of one [BK][256] operand image: a per-lane byte offset relative to the K-tile's
+// first element (source-permuted swizzle), issued with the tile offset as the scalar soffset.  Piece i covers rows
+// 2 (wave + NW i) + {0, 1}: the row advances by 2 NW (a multiple of 8), so the swizzle is the same for every piece
+// and piece i only adds i * step bytes to the scalar offset (one VGPR per operand instead of NP).
 template <int NP, int NW = kWaves>
 struct Dma {
-    int voff[NP];
+    static_assert(NW % 4 == 0, "piece rows must advance by a multiple of 8 for a piece-invariant swizzle");
+    int voff;
+    int step;
     __device__ __forceinline__ void init(int wave, int lane, int ld) {
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            const int piece = wave + NW * i;
-            const int row = 2 * piece + (lane >> 5);
-            const int slot = (lane & 31) ^ ((row & 3) << 2);
-            voff[i] = (row * ld + slot * 8) * 2;
-        }
+        const int row = 2 * wave + (lane >> 5);
+        const int slot = (lane & 31) ^ ((row & 3) << 2);
+        voff = (row * ld + slot * 8) * 2;
+        step = __builtin_amdgcn_readfirstlane(4 * NW * ld);
     }
     // Issued as inline asm on purpose: for a compiler-visible LDS-DMA the waitcnt pass cannot tell which LDS
     // bytes are pending and puts s_waitcnt vmcnt(0) in front of every later ds_read, draining the whole
@@ -89,7 +90,7 @@ struct Dma {
             "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(saved)
-            : "s"(lds), "v"(voff[i]), "s"(rs), "s"(soff)
+            : "s"(lds), "v"(voff), "s"(rs), "s"(soff + i * step)
             : "memory");
     }
     __device__ __forceinline__ void load(const void* base, uint32_t nbytes, int soff, char* img, int wave_u) const {
@@ -111,7 +112,7 @@ struct Dma {
                 "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
                 "s_mov_b32 m0, %0"
                 : "=&s"(saved)
-                : "s"(lds0 + i * NW * 1024), "v"(voff[i]), "s"(rs), "s"(soff)
+                : "s"(lds0 + i * NW * 1024), "v"(voff), "s"(rs), "s"(soff + i * step)
                 : "memory");
         }
     }
@@ -146,7 +147,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
                                                          float* __restrict__ ws) {
     using G = Cfg<BK>;
     constexpr int KS = BK / 16;                   // MFMA k-steps per K-tile
-    constexpr bool SPLIT = STAGES == 2;           // group 0 stages A images, group 1 stages B images
+    constexpr bool B3 = STAGES == 3;              // two A buffers + three B buffers (160 KiB): see below
+    constexpr bool SPLIT = STAGES == 2 || B3;     // group 0 stages A images, group 1 stages B images
     constexpr int NW = SPLIT ? kWaves / 2 : kWaves;  // waves staging one image
     constexpr int NP = G::kImg / 1024 / NW;       // LDS-DMA instructions per staging wave per operand image
     constexpr int PT = SPLIT ? NP : 2 * NP;       // ... per K-tile
@@ -206,16 +208,21 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
         else wait_vm<0>();                                                                                \
     }
     if constexpr (SPLIT) {
+        // B3 (variant 5): A images rotate over two buffers, B images over three (2 x 32 + 3 x 32 KiB = all of LDS).
+        // Group 1 then stages tile t+2's B image in its READ window of phase t (buffer (t+2) % 3 = (t-1) % 3, whose
+        // last reads retired before event 2t) and retires it one read window later (before event 2t+4, where group
+        // 0 starts reading it): no LDS-DMA issue inside any MFMA window, and B gets two phases of latency cover.
         // Two stages.  Group 0 stages tile t+1's A image at the start of its read window of phase t and retires
         // it behind its MFMAs (before barrier event 2t+2); group 1 stages tile t+2's B image inside its MFMA
         // window of phase t (event 2t+2 onward: both groups' reads of tile t are retired by then) and retires it
         // in its read window of phase t+1 (before event 2t+4).  Each wave has at most one image in flight.
+#define SA_ABUF(t_) (B3 ? smem + ((t_) & 1) * G::kImg : smem + ((t_) & 1) * G::kStage)
+#define SA_BBUF(t_) (B3 ? smem + (2 + (t_) % 3) * G::kImg : smem + ((t_) & 1) * G::kStage + G::kImg)
 #define SA_ISSUE_G(t_)                                                                                    \
         {                                                                                                 \
-            char* st_ = smem + ((t_) & 1) * G::kStage;                                                    \
             const int k0_ = (k_lo + (t_)) * BK;                                                                    \
-            if (wm == 0) da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), st_, swave); \
-            else db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), st_ + G::kImg, swave); \
+            if (wm == 0) da.load(A, a_bytes, __builtin_amdgcn_readfirstlane((k0_ * lda + m0) * 2), SA_ABUF(t_), swave); \
+            else db.load(B, b_bytes, __builtin_amdgcn_readfirstlane((k0_ * ldb + n0) * 2), SA_BBUF(t_), swave); \
         }
         SA_ISSUE_G(0)
         if (wm == 1 && nk > 1) {
@@ -227,8 +234,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
         hard_barrier();
         if (wm == 1) hard_barrier();
         for (int t = 0; t < nk; ++t) {
-            const char* ia = smem + (t & 1) * G::kStage;
-            const char* ib = ia + G::kImg;
+            const char* ia = SA_ABUF(t);
+            const char* ib = SA_BBUF(t);
             uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + STAGES * G::kStage) +
                               (wave * kDbgTiles + (t - kDbgT0)) * kDbgEv;
             const bool rec = TIMING && blockIdx.x == 0 && t >= kDbgT0 && t < kDbgT0 + kDbgTiles && lane == 0;
@@ -243,7 +250,16 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
 #pragma unroll
                 for (int j = 0; j < 2; ++j) b[ks][j] = frag_tr(ib, 16 * ks, 64 * wn + 32 * j, lane);
             }
-            if (t + 1 < nk) {
+            if constexpr (B3) {
+                if (wm == 0) {
+                    if (t + 1 < nk) SA_ISSUE_G(t + 1)
+                } else if (t + 2 < nk) {
+                    SA_ISSUE_G(t + 2)
+                    wait_vm<NP>();  // B(t+1) retired, B(t+2) stays in flight
+                } else {
+                    wait_vm<0>();
+                }
+            } else if (t + 1 < nk) {
                 if (wm == 0) SA_ISSUE_G(t + 1)
                 else wait_vm<0>();
             }
@@ -254,7 +270,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
             __builtin_amdgcn_s_setprio(1);
             // group 1 threads its B-image pieces for tile t+2 between the MFMAs (one per 32 / NP MFMAs) so
             // they issue in the matrix pipe's shadow
-            const bool stage_b = wm == 1 && t + 2 < nk;
+            const bool stage_b = !B3 && wm == 1 && t + 2 < nk;
             const int soff_b = __builtin_amdgcn_readfirstlane(((k_lo + t + 2) * BK * ldb + n0) * 2);
             char* st_b = smem + (t & 1) * G::kStage + G::kImg;
 #pragma unroll
@@ -281,6 +297,8 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const u16* __restrict__
         }
 #undef SA_STAMP
 #undef SA_ISSUE_G
+#undef SA_ABUF
+#undef SA_BBUF
     } else {
     // prologue: LEAD K-tiles in flight, tile 0 retired, group 1 one barrier behind
 #pragma unroll
@@ -407,13 +425,10 @@ __device__ __forceinline__ bf16x8 frag16_tr(const char* img, int kb, int c0, int
 template <int NP, int NW>
 struct Dma16 : Dma<NP, NW> {
     __device__ __forceinline__ void init(int wave, int lane, int ld) {
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            const int piece = wave + NW * i;
-            const int row = 2 * piece + (lane >> 5);
-            const int slot = (lane & 31) ^ sw16(row);
-            this->voff[i] = (row * ld + slot * 8) * 2;
-        }
+        const int row = 2 * wave + (lane >> 5);
+        const int slot = (lane & 31) ^ sw16(row);
+        this->voff = (row * ld + slot * 8) * 2;
+        this->step = __builtin_amdgcn_readfirstlane(4 * NW * ld);
     }
 };
 
@@ -553,6 +568,7 @@ template __global__ void gemm_tn16_kernel<false>(const u16* __restrict__, int, u
                                                                  uint64_t* __restrict__, int, int, float* __restrict__);
 #define SA_GEMM_INST2(BK, S, LW) SA_GEMM_INST(true, BK, S, LW, false) SA_GEMM_INST(false, BK, S, LW, false)
 SA_GEMM_INST2(32, 4, false) SA_GEMM_INST2(32, 4, true) SA_GEMM_INST2(64, 2, true) SA_GEMM_INST2(32, 5, true)
+SA_GEMM_INST2(64, 3, true)
 SA_GEMM_INST(false, 32, 4, true, true) SA_GEMM_INST(false, 64, 2, true, true)
 #undef SA_GEMM_INST2
 #undef SA_GEMM_INST
@@ -589,7 +605,8 @@ void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, 
     if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
     const int grid = full_blocks + (nwg - full_blocks) * split;
     const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
-    hipLaunchKernelGGL((gemm_tn_kernel<BETA, BK, STAGES, LW>), dim3(grid), dim3(512), STAGES * Cfg<BK>::kStage, st,
+    const int lds = (BK == 64 && STAGES == 3) ? 5 * Cfg<BK>::kImg : STAGES * Cfg<BK>::kStage;
+    hipLaunchKernelGGL((gemm_tn_kernel<BETA, BK, STAGES, LW>), dim3(grid), dim3(512), lds, st,
                        (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
                        (int)K, nullptr, full_blocks, split, ws);
     if (split > 1)
@@ -602,7 +619,8 @@ using namespace sa_gemm;
 
 namespace sa_launch {
 // pipeline variants (benchmarking hook): 2 (default) = BK 64 x 2 stages, split staging (one 32-MFMA block per
-// phase); 0 = BK 32 x 4 stages, wait behind the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages
+// phase); 5 = the same with three B buffers (B staged in group 1's read window); 0 = BK 32 x 4 stages, wait behind
+// the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2
 static int g_gemm_variant = 2;
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 // profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
@@ -634,7 +652,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     const int nwg = (int)((M / 256) * (N / 256));
     full_blocks = nwg;
     split = 1;
-    if (g_gemm_variant != 2 || slots <= 0) return 0;
+    if ((g_gemm_variant != 2 && g_gemm_variant != 5) || slots <= 0) return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
     if (r == 0) return 0;
     // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
@@ -655,6 +673,11 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
     if (g_gemm_variant == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        return;
+    }
+    if (g_gemm_variant == 5) {
+        if (beta) launch_tn<true, 64, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        else launch_tn<false, 64, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
 #define SA_TN(BK, S, LW)                                                                      \

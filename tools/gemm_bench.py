@@ -33,6 +33,7 @@ def main() -> None:
     ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", type=str, default="", help="comma list of gemm_tn pipeline variants to compare")
+    ap.add_argument("--rounds", type=int, default=5, help="interleaved timing rounds per variant (median reported)")
     a = ap.parse_args()
     T = a.tokens
     out = {}
@@ -48,12 +49,22 @@ def main() -> None:
         ext().gemm_tn(g, x, c2, True)
         err_acc = ((c2.float() - 2 * ref).abs().max() / ref.abs().max()).item()
         r = {}
-        for vv in [int(t) for t in a.variants.split(",") if t]:
+        vs = [int(t) for t in a.variants.split(",") if t]
+        for vv in vs:
             ext().gemm_set_variant(vv)
             cv = torch.zeros_like(c)
             ext().gemm_tn(g, x, cv, False)
-            r[f"v{vv}" + ("b" if f"v{vv}" in r else "")] = fl / timeit(lambda: ext().gemm_tn(g, x, cv, False), a.iters) / 1e12
             r[f"v{vv}_err"] = ((cv.float() - ref).abs().max() / ref.abs().max()).item()
+            ca = c.clone()
+            ext().gemm_tn(g, x, ca, True)
+            r[f"v{vv}_err_acc"] = ((ca.float() - 2 * ref).abs().max() / ref.abs().max()).item()
+        samples: dict = {vv: [] for vv in vs}
+        for _ in range(a.rounds if vs else 0):  # interleaved rounds: variants see the same clock drift
+            for vv in vs:
+                ext().gemm_set_variant(vv)
+                samples[vv].append(fl / timeit(lambda: ext().gemm_tn(g, x, c, True), a.iters) / 1e12)
+        for vv in vs:
+            r[f"v{vv}"] = sorted(samples[vv])[len(samples[vv]) // 2]
         ext().gemm_set_variant(2)
         r.update({
             "ours": fl / timeit(lambda: ext().gemm_tn(g, x, c, False), a.iters) / 1e12,
