@@ -6,6 +6,8 @@
 //   O^T += V^T P^T (P^T accumulators reused as B operands; V^T via ds_read_b64_tr_b16)
 // GQA is native (kv head = q head / group); varlen via cu_seqlens; causal (bottom-right aligned,
 // flash-attn convention) and sliding window.
+#include <cstdlib>
+
 #include "flash_attn.h"
 #include "launch.h"
 
@@ -181,16 +183,18 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 //    representable in bf16);
 //  * lane^32 exchanges through v_permlane32_swap;
 //  * masking only on boundary tiles, as 1-2 compares against per-lane bounds.
-template <int D>
+template <int D, int NW_ = 8>
 struct FwdV2 {
-    static constexpr int NW = 8, BM = 32 * NW, KT = 64, TILE = KT * D * 2, NKS = D / 16, NT = D / 32;
+    static constexpr int NW = NW_, BM = 32 * NW, KT = 64, TILE = KT * D * 2, NKS = D / 16, NT = D / 32;
     static constexpr float TH = 8.f;
 };
 
-template <int D, bool F16, bool DROP>
-__global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
+// NW = 8: one 512-thread workgroup per CU; NW = 4: two independent 256-thread workgroups per CU (their phases
+// drift apart, so one workgroup's softmax can overlap the other's MFMAs on a SIMD)
+template <int D, bool F16, bool DROP, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
-    using C = FwdV2<D>;
+    using C = FwdV2<D, NW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
     // dimension and causal work is issued heaviest-first across all heads (LPT balance)
@@ -386,6 +390,16 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_v2_kernel(FwdArgs a) {
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
+        static const int nw = [] {
+            const char* e = getenv("SCALING_AMD_FA_FWD_WAVES");  // 4 (default, measured faster) or 8
+            return e && atoi(e) == 8 ? 8 : 4;
+        }();
+        if (nw == 4) {
+            dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128, 4>::BM - 1) / FwdV2<128, 4>::BM), block(256);
+            if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+            else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, 4>), grid, block, 4 * FwdV2<64>::TILE, st, a);
+            return;
+        }
         dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(64 * FwdV2<128>::NW);
         if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
         else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
