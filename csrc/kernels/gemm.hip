@@ -93,6 +93,28 @@ struct Dma {
             : "s"(lds), "v"(voff), "s"(rs), "s"(soff + i * step)
             : "memory");
     }
+    // the same piece without a "memory" clobber, for a caller whose barriers (asm with a memory clobber) already
+    // order it after the last reads of its destination: with the clobber the waitcnt pass drains every pending LDS
+    // read (lgkmcnt(0)) right behind the asm
+    __device__ __forceinline__ void load_piece_nc(int i, const void* base, uint32_t nbytes, int soff, char* img,
+                                                  int wave_u) const {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const uint64_t a = reinterpret_cast<uint64_t>(base);
+        const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
+                          (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffff),
+                          (int)__builtin_amdgcn_readfirstlane(nbytes), fa::kBufFlags};
+        const uint32_t lds = __builtin_amdgcn_readfirstlane(
+            (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)(img + (wave_u + NW * i) * 1024)));
+        int saved;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %1\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(saved)
+            : "s"(lds), "v"(voff), "s"(rs), "s"(soff + i * step));
+    }
     __device__ __forceinline__ void load(const void* base, uint32_t nbytes, int soff, char* img, int wave_u) const {
         typedef int i32x4 __attribute__((ext_vector_type(4)));
         const uint64_t a = reinterpret_cast<uint64_t>(base);
@@ -559,6 +581,208 @@ template __global__ void gemm_tn16_kernel<true>(const u16* __restrict__, int, ui
 template __global__ void gemm_tn16_kernel<false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
                                                  uint32_t, u16* __restrict__, int, int, int, int);
 
+// ---------------------------------------------------------------------------------------------------------------
+// Variant 6: no ping-pong.  Every wave interleaves its own fragment reads with its MFMAs (the reads of k-step ks+1
+// issue in the shadow of k-step ks's 8 MFMAs), so both waves of a SIMD feed the matrix pipe all the time instead of
+// alternating a 32-MFMA window with a read window.  One barrier per 64-deep K-tile, placed before the tile's last
+// k-step: by then every wave has retired its reads of the tile and its LDS-DMA pieces of the next one, so right after
+// it each wave (a) reads the next tile's first fragments and (b) threads its pieces of tile t+2 (into the buffer
+// just released) between the last k-step's MFMAs — the barrier's read latency hides behind those MFMAs.
+//   LDS 2 x 64 KiB; every wave stages NP = 4 pieces of each operand image per K-tile.
+template <bool BETA, bool TIMING = false>
+__global__ __launch_bounds__(512, 1) void gemm_tn_il_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                            const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                            u16* __restrict__ C, int ldc, int M, int N, int K,
+                                                            int full_blocks, int tail_split, float* __restrict__ ws,
+                                                            uint64_t* __restrict__ dbg = nullptr) {
+    constexpr int BK = 64;
+    using G = Cfg<BK>;
+    constexpr int NP = G::kImg / 1024 / kWaves;  // LDS-DMA pieces per wave per operand image (4)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+
+    const int tm = M / 256, tn = N / 256;
+    int v, k_lo = 0, nk = K / BK, unit = -1;
+    if ((int)blockIdx.x < full_blocks) {
+        v = xcd_remap(blockIdx.x, full_blocks);
+    } else {
+        unit = (int)blockIdx.x - full_blocks;
+        v = full_blocks + unit / tail_split;
+        nk /= tail_split;
+        k_lo = (unit % tail_split) * nk;
+    }
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    Dma<NP, kWaves> da, db;
+    da.init(wave, lane, lda);
+    db.init(wave, lane, ldb);
+
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    bf16x8 fa[2][4], fb[2][2];
+#define SA_IL_READ(IA, IB, KS, SET)                                                                     \
+    {                                                                                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) fa[SET][i] = frag_tr((IA), 16 * (KS), 128 * wm + 32 * i, lane); \
+        _Pragma("unroll") for (int j = 0; j < 2; ++j) fb[SET][j] = frag_tr((IB), 16 * (KS), 64 * wn + 32 * j, lane);  \
+    }
+#define SA_IL_MFMA(SET)                                                                                 \
+    {                                                                                                   \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                   \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j) acc[i][j] = fa::mfma(fb[SET][j], fa[SET][i], acc[i][j]); \
+    }
+    // 8 MFMAs of the current k-step with the 12 reads of the next one threaded between them
+#define SA_IL_SCHED()                                                       \
+    {                                                                       \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                     \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              \
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);              \
+        }                                                                   \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q) {                     \
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              \
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);              \
+        }                                                                   \
+    }
+    auto soff_a = [&](int t) { return __builtin_amdgcn_readfirstlane(((k_lo + t) * BK * lda + m0) * 2); };
+    auto soff_b = [&](int t) { return __builtin_amdgcn_readfirstlane(((k_lo + t) * BK * ldb + n0) * 2); };
+
+    // prologue: tiles 0 and 1 in flight, tile 0 retired, its first fragments requested
+    da.load(A, a_bytes, soff_a(0), smem, wave);
+    db.load(B, b_bytes, soff_b(0), smem + G::kImg, wave);
+    if (nk > 1) {
+        da.load(A, a_bytes, soff_a(1), smem + G::kStage, wave);
+        db.load(B, b_bytes, soff_b(1), smem + G::kStage + G::kImg, wave);
+        wait_vm<2 * NP>();
+    } else {
+        wait_vm<0>();
+    }
+    hard_barrier();
+    SA_IL_READ(smem, smem + G::kImg, 0, 0)
+    for (int t = 0; t < nk; ++t) {
+        const char* ia = smem + (t & 1) * G::kStage;
+        const char* ib = ia + G::kImg;
+        // timing build: events per K-tile 0 top, 1 k-steps 0-2 issued, 2 reads + DMA retired, 3 past the barrier,
+        // 4 last k-step issued (stamps of workgroup 0 in LDS past the two stages)
+        uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + 2 * G::kStage) + (wave * kDbgTiles + (t - kDbgT0)) * kDbgEv;
+        const bool rec = TIMING && blockIdx.x == 0 && t >= kDbgT0 && t < kDbgT0 + kDbgTiles && lane == 0;
+#define SA_IL_STAMP(e_) \
+        if (rec) stamp[e_] = __builtin_amdgcn_s_memtime();
+        SA_IL_STAMP(0)
+        SA_IL_READ(ia, ib, 1, 1)
+        SA_IL_MFMA(0)
+        SA_IL_SCHED()
+        SA_IL_READ(ia, ib, 2, 0)
+        SA_IL_MFMA(1)
+        SA_IL_SCHED()
+        SA_IL_READ(ia, ib, 3, 1)
+        SA_IL_MFMA(0)
+        SA_IL_SCHED()
+        // every read of buffer t&1 retired (compiler-visible wait, so its own lgkm bookkeeping stays exact), this
+        // wave's pieces of tile t+1 landed -> publish
+        SA_IL_STAMP(1)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        wait_vm<0>();
+        SA_IL_STAMP(2)
+        hard_barrier();
+        SA_IL_STAMP(3)
+        {  // next tile's first fragments (after the last tile: a harmless read of the other buffer, never used)
+            const char* na = smem + ((t + 1) & 1) * G::kStage;
+            SA_IL_READ(na, na + G::kImg, 0, 0)
+        }
+        // last k-step of tile t; tile t+2's pieces (into the buffer just released) threaded between its MFMAs
+        const bool stage = t + 2 < nk;
+        char* st = smem + (t & 1) * G::kStage;
+        const int sa = soff_a(t + 2), sb = soff_b(t + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc[i][j] = fa::mfma(fb[1][j], fa[1][i], acc[i][j]);
+                const int m = i * 2 + j;  // 8 MFMAs, 8 pieces: A pieces after even, B pieces after odd MFMAs
+                if (stage) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if ((m & 1) == 0) da.load_piece_nc(m >> 1, A, a_bytes, sa, st, wave);
+                    else db.load_piece_nc(m >> 1, B, b_bytes, sb, st + G::kImg, wave);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        SA_IL_STAMP(4)
+#undef SA_IL_STAMP
+    }
+    if (TIMING && blockIdx.x == 0) {
+        __syncthreads();
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(smem + 2 * G::kStage);
+        for (int i = threadIdx.x; i < kWaves * kDbgTiles * kDbgEv; i += blockDim.x) dbg[i] = src[i];
+    }
+#undef SA_IL_READ
+#undef SA_IL_MFMA
+#undef SA_IL_SCHED
+
+    const int h = lane >> 5, c = lane & 31;
+    if (unit >= 0) {  // K-slice of a tail tile: fp32 partial [256][256] at ws + unit * 65536
+        float* wp = ws + (int64_t)unit * 65536;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float* rp = wp + (128 * wm + 32 * i + c) * 256 + 64 * wn + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f32x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(rp + 32 * j + 8 * q) = o;
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 32 * i + c) * ldc + n0 + 64 * wn + 4 * h;
+        u16x4 old[2][4];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) old[j][q] = *reinterpret_cast<const u16x4*>(crow_p + 32 * j + 8 * q);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = acc[i][j][4 * q + e];
+                    if (BETA) x += bf2f(old[j][q][e]);
+                    o[e] = f2bf(x);
+                }
+                *reinterpret_cast<u16x4*>(crow_p + 32 * j + 8 * q) = o;
+            }
+    }
+}
+template __global__ void gemm_tn_il_kernel<true, false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                        int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
+                                                        float* __restrict__, uint64_t* __restrict__);
+template __global__ void gemm_tn_il_kernel<false, false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                         int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
+                                                         float* __restrict__, uint64_t* __restrict__);
+template __global__ void gemm_tn_il_kernel<false, true>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                        int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
+                                                        float* __restrict__, uint64_t* __restrict__);
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -598,6 +822,21 @@ __global__ __launch_bounds__(256) void gemm_tn_combine_kernel(const float* __res
     *reinterpret_cast<u16x4*>(cp) = o;
 }
 
+template <bool BETA>
+void launch_tn_il(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+                  int64_t K, hipStream_t st, int full_blocks, int split, float* ws) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
+    const int grid = full_blocks + (nwg - full_blocks) * split;
+    const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+    hipLaunchKernelGGL((gemm_tn_il_kernel<BETA, false>), dim3(grid), dim3(512), 2 * Cfg<64>::kStage, st, (const u16*)A,
+                       (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, full_blocks,
+                       split, ws, nullptr);
+    if (split > 1)
+        hipLaunchKernelGGL(gemm_tn_combine_kernel, dim3(nwg - full_blocks, 64), dim3(256), 0, st, (const float*)ws, (u16*)C,
+                           (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
+}
+
 template <bool BETA, int BK, int STAGES, bool LW>
 void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                int64_t K, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr) {
@@ -620,7 +859,8 @@ using namespace sa_gemm;
 namespace sa_launch {
 // pipeline variants (benchmarking hook): 2 (default) = BK 64 x 2 stages, split staging (one 32-MFMA block per
 // phase); 5 = the same with three B buffers (B staged in group 1's read window); 0 = BK 32 x 4 stages, wait behind
-// the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2
+// the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2;
+// 6 = no ping-pong, reads interleaved with each wave's own MFMAs (gemm_tn_il_kernel)
 static int g_gemm_variant = 2;
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 // profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
@@ -629,7 +869,11 @@ void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void
     const int nwg = (int)((M / 256) * (N / 256));
     const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
     const int extra = kWaves * kDbgTiles * kDbgEv * 8;
-    if (g_gemm_variant == 2)
+    if (g_gemm_variant == 6)
+        hipLaunchKernelGGL((gemm_tn_il_kernel<false, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra, st,
+                           (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
+                           (int)K, nwg, 1, nullptr, dbg);
+    else if (g_gemm_variant == 2)
         hipLaunchKernelGGL((gemm_tn_kernel<false, 64, 2, true, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra,
                            st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M,
                            (int)N, (int)K, dbg, nwg, 1, nullptr);
@@ -652,7 +896,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     const int nwg = (int)((M / 256) * (N / 256));
     full_blocks = nwg;
     split = 1;
-    if ((g_gemm_variant != 2 && g_gemm_variant != 5) || slots <= 0) return 0;
+    if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6) || slots <= 0) return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
     if (r == 0) return 0;
     // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
@@ -673,6 +917,11 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
     if (g_gemm_variant == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        return;
+    }
+    if (g_gemm_variant == 6) {
+        if (beta) launch_tn_il<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        else launch_tn_il<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
     if (g_gemm_variant == 5) {

@@ -477,12 +477,12 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 4, 5])
+@pytest.mark.parametrize("variant", [2, 4, 5, 6])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
 def test_gemm_tn(M, N, K, accumulate, variant):
     """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands; pipeline
-    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA) and 5 (three B buffers)."""
+    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers) and 6 (no ping-pong)."""
     ext().gemm_set_variant(variant)
     try:
         _gemm_tn_case(M, N, K, accumulate)

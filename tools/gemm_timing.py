@@ -38,4 +38,7 @@ for rep in range(3):
         b1 = (sub[:, :, 2] - sub[:, :, 1]).mean()
         m = (sub[:, :, 3] - sub[:, :, 2]).mean()
         b2 = (sub[:, :, 4] - sub[:, :, 3]).mean()
-        print(f"  group {grp}: reads+dma {r:.1f}  barrier1 {b1:.1f}  mfma-issue {m:.1f}  barrier2 {b2:.1f}")
+        if os.environ.get("GEMM_VARIANT", "2") == "6":
+            print(f"  group {grp}: ksteps0-2 {r:.1f}  waits(lgkm+vm) {b1:.1f}  barrier {m:.1f}  kstep3+dma {b2:.1f}")
+        else:
+            print(f"  group {grp}: reads+dma {r:.1f}  barrier1 {b1:.1f}  mfma-issue {m:.1f}  barrier2 {b2:.1f}")
