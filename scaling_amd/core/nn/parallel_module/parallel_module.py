@@ -392,6 +392,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         self.pipe_buffer.write(BufferType.PIPELINE_STAGE_OUTPUT, buffer_id, None)
 
     def _execute_backward_pass(self, buffer_id: int, optimizer: BaseOptimizer) -> None:
+        optimizer.wait_grad_zeroing()  # an overlapped optimizer step zeroes the gradient buffers on its stream
         if self.topology.is_last_pipe_parallel_rank:
             optimizer.backward(self.pipe_buffer.take(BufferType.LOSS, buffer_id))
         else:

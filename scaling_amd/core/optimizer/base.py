@@ -60,3 +60,7 @@ class BaseOptimizer(ABC):
 
     def wait_param_sync(self, layer: Optional[Any] = None) -> None:
         pass
+
+    def wait_grad_zeroing(self) -> None:
+        """Makes the current stream wait for an asynchronous gradient zeroing (overlapped step); default no-op."""
+        return None

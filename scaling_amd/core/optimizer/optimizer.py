@@ -19,10 +19,15 @@ MI355X-first differences:
 * with ZeRO the parameter all-gather of bucket b is issued on the side stream right after bucket b's
   AdamW and completes asynchronously: each pipeline layer's next forward waits only for the buckets
   holding its parameters (``attach_param_sync``/``wait_param_sync``), so the gather of late layers
-  overlaps the forward of early ones.
+  overlaps the forward of early ones;
+* the update itself (``overlap_optimizer_step``) runs on that side stream too: bucket by bucket, the
+  smallest parameter group (norms) first so layer 0 is ready early, then the gradient zeroing; the next
+  forward waits per layer, the next backward for the zeroing.  The bandwidth-bound AdamW passes overlap
+  the compute-bound forward GEMMs of the next step instead of running between the two.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from pathlib import Path
 from typing import Any, Optional, Union
@@ -70,6 +75,8 @@ class Optimizer(BaseOptimizer):
         self._armed = False
         self._deferred = self._deferred_buckets()
         self._ag_events: dict[tuple[int, int], Any] = {}
+        self._side_stream: Optional[Any] = None  # overlapped optimizer step without a DP comm stream
+        self._zero_event: Optional[Any] = None  # gradient zeroing of the last overlapped step
         self._layer_buckets: dict[int, list[tuple[int, int]]] = {}
         self._hooks = []
         if self.dp > 1 and config.overlap_grad_reduce and not topology.config.sequence_parallel:
@@ -191,6 +198,7 @@ class Optimizer(BaseOptimizer):
             g.zero_grad(set_to_none)
 
     def backward(self, loss: torch.Tensor) -> None:
+        self.wait_grad_zeroing()
         loss = loss.float()
         if self.topology.config.gradient_accumulation_steps > 1:
             loss = loss / self.topology.config.gradient_accumulation_steps
@@ -216,6 +224,23 @@ class Optimizer(BaseOptimizer):
         v = vals.tolist()
         return float(v[0]), float(v[1])
 
+    # ------------------------------------------------------------------ overlapped optimizer step
+    def _async_step(self) -> bool:
+        return bool(self._gpu and self.config.overlap_optimizer_step)
+
+    def _step_stream(self) -> Any:
+        if self._comm_stream is not None:  # AdamW then the ZeRO all-gather of the bucket, in order, on one stream
+            return self._comm_stream
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=self.topology.device)
+        return self._side_stream
+
+    def wait_grad_zeroing(self) -> None:
+        """The gradient buffers are zeroed on the side stream by an overlapped step: wait before writing them."""
+        if self._zero_event is not None:
+            torch.cuda.current_stream(self.topology.device).wait_event(self._zero_event)
+            self._zero_event = None
+
     # ------------------------------------------------------------------ parameter all-gather overlap
     def _async_param_gather(self) -> bool:
         return bool(self.config.zero and self.dp > 1 and self._comm_stream is not None and self.config.overlap_param_gather)
@@ -232,7 +257,9 @@ class Optimizer(BaseOptimizer):
             self._layer_buckets[id(layer)] = keys
 
     def wait_param_sync(self, layer: Optional[Any] = None) -> None:
-        """Makes the current stream wait for the pending all-gathers of `layer`'s buckets (all if None)."""
+        """Makes the current stream wait for the pending updates / all-gathers of `layer`'s buckets (all if None)."""
+        if layer is None:
+            self.wait_grad_zeroing()
         if not self._ag_events:
             return
         if layer is None:
@@ -289,23 +316,43 @@ class Optimizer(BaseOptimizer):
         for gi, g in enumerate(self.parameter_groups):
             g.lr = g.learning_rate_scheduler.get_lr(step_index=self.step_index)
             g.adam_step += 1
-            src = g.grad_source()
-            for b in range(g.num_buckets):
-                if g.owned_grad is not None:
-                    gb = g.owned_view(src, b)
-                else:
-                    s = g.owned_flat_starts[b]
-                    gb = src[s : s + g.chunk]
-                optim_ops.adamw_step_(
-                    g.owned_view(g.master, b), gb, g.owned_view(g.exp_avg, b), g.owned_view(g.exp_avg_sq, b),
-                    lr=g.lr, beta1=self.config.beta1, beta2=self.config.beta2, eps=self.config.eps,
-                    weight_decay=g.config.weight_decay, step=g.adam_step, grad_scale=gscale,
-                    param_out=g.param_chunk_view(b),
-                )
-                if self.config.zero and self.dp > 1:
-                    self._gather_bucket(g, gi, b)
             learning_rates[g.config.name or f"parameter_group_{gi}"] = g.lr
-        self.zero_grad()
+        overlap = self._async_step()
+        ctx: Any = contextlib.nullcontext()
+        if overlap:
+            side = self._step_stream()
+            side.wait_stream(torch.cuda.current_stream(self.topology.device))
+            ctx = torch.cuda.stream(side)
+        # smallest group first (norm weights / biases of every layer), then the large one bucket by bucket in
+        # parameter order, so the first layers' parameters are final first
+        order = sorted(range(len(self.parameter_groups)),
+                       key=lambda i: self.parameter_groups[i].num_buckets * self.parameter_groups[i].bucket_size)
+        with ctx:
+            for gi in order:
+                g = self.parameter_groups[gi]
+                src = g.grad_source()
+                for b in range(g.num_buckets):
+                    if g.owned_grad is not None:
+                        gb = g.owned_view(src, b)
+                    else:
+                        s = g.owned_flat_starts[b]
+                        gb = src[s : s + g.chunk]
+                    optim_ops.adamw_step_(
+                        g.owned_view(g.master, b), gb, g.owned_view(g.exp_avg, b), g.owned_view(g.exp_avg_sq, b),
+                        lr=g.lr, beta1=self.config.beta1, beta2=self.config.beta2, eps=self.config.eps,
+                        weight_decay=g.config.weight_decay, step=g.adam_step, grad_scale=gscale,
+                        param_out=g.param_chunk_view(b),
+                    )
+                    if self.config.zero and self.dp > 1:
+                        self._gather_bucket(g, gi, b)
+                    if overlap and (gi, b) not in self._ag_events:
+                        ev = torch.cuda.Event()
+                        ev.record(torch.cuda.current_stream(self.topology.device))
+                        self._ag_events[(gi, b)] = ev
+            self.zero_grad()
+            if overlap:
+                self._zero_event = torch.cuda.Event()
+                self._zero_event.record(torch.cuda.current_stream(self.topology.device))
         invalidate_transposed_weights()
         return OptimizerStepOutput(global_grad_norm, None, learning_rates, ls_out.overflow, ls_out.no_overflow_steps,
                                    ls_out.current_loss_scale, debug_dict)

@@ -26,6 +26,11 @@ class OptimizerConfig(BaseConfig):
         "float32", description="dtype of the data-parallel gradient reduction ('float32' as the reference, or 'bfloat16')"
     )
     overlap_grad_reduce: bool = Field(True, description="overlap the data-parallel gradient reduction with backward")
+    overlap_optimizer_step: bool = Field(
+        True,
+        description="run the AdamW update (and the ZeRO all-gather) bucket by bucket on a side stream; the next "
+        "forward waits per layer for its buckets, the next backward for the gradient zeroing (GPU only)",
+    )
     overlap_param_gather: bool = Field(
         True,
         description="ZeRO: all-gather updated parameters bucket by bucket on a side stream and let each pipeline "
