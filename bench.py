@@ -45,10 +45,13 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--model", type=str, default="llama2_7b")
     p.add_argument("--seq-len", type=int, default=4096)
-    # 8 sequences of 4096 tokens per GPU per step; 4 x 2 measured +2.8 % over 2 x 4 (bigger GEMMs, fewer
-    # weight-gradient read-modify-writes; profiles/bench_7b_r2_microbatch_ab.log)
-    p.add_argument("--micro-batch", type=int, default=4)
-    p.add_argument("--grad-acc", type=int, default=2)
+    # 8 sequences of 4096 tokens per GPU per step.  4 x 2 measured +2.8 % over 2 x 4 (bigger GEMMs, fewer
+    # weight-gradient read-modify-writes; profiles/bench_7b_r2_microbatch_ab.log); 8 x 1 with the 32k-token
+    # GEMMs in the tuned table another +0.6 % (profiles/bench_7b_r2i_mb8_ab.log, peak 230 GiB of 288 at one GPU)
+    # and, with data parallelism, the gradient reduce-scatter overlaps the whole backward instead of the last
+    # micro-batch's
+    p.add_argument("--micro-batch", type=int, default=8)
+    p.add_argument("--grad-acc", type=int, default=1)
     p.add_argument("--tp", type=int, default=1)
     p.add_argument("--pp", type=int, default=1)
     p.add_argument("--activation-checkpointing", type=str, default="disabled",
