@@ -60,6 +60,8 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--zero", type=int, default=1)
     p.add_argument("--overlap-step", type=int, default=1,
                    help="run the optimizer update on a side stream, overlapped with the next forward (1) or inline (0)")
+    p.add_argument("--lazy-zero", type=int, default=1,
+                   help="optimizer lazy_grad_zeroing: no per-step gradient memset, first weight-gradient GEMM writes")
     p.add_argument("--lora", action="store_true",
                    help="LoRA finetune path (BASELINE #5): q/k/v/dense adapters trained, base weights frozen")
     p.add_argument("--lora-rank", type=int, default=64)
@@ -186,7 +188,7 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
     return {
         "topology": topo,
         "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero),
-                      "overlap_optimizer_step": bool(a.overlap_step)},
+                      "overlap_optimizer_step": bool(a.overlap_step), "lazy_grad_zeroing": bool(a.lazy_zero)},
         "learning_rate_scheduler": {"learning_rate": 3e-4, "learning_rate_minimum": 3e-5,
                                     "learning_rate_decay_style": "cosine", "learning_rate_warmup_steps": 2,
                                     "learning_rate_decay_iters": 1000},

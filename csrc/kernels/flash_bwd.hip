@@ -139,8 +139,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     DmaTile<D, 4, QT> tq, td;
     tq.init(wave, lane, a.q_tok);
     td.init(wave, lane, a.do_tok);
-    auto issue = [&](int w, char* buf) {
-        const int gi = w / ntq, qt = qlo + (w % ntq) * QT, hq = h0 + gi;
+    // work item (q head h0 + gi, query tile qlo + QT qi), qi fastest; the issue and compute cursors advance
+    // incrementally (no runtime divisions in the loop)
+    auto issue = [&](int gi, int qi, char* buf) {
+        const int qt = qlo + qi * QT, hq = h0 + gi;
         dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
         dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
         if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
@@ -155,14 +157,14 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     for (int t = 0; t < NT; ++t) { dk[t] = f32x16{}; dv[t] = f32x16{}; }
     const float c2 = a.scale_log2;
 
-    auto tile = [&](const char* Q, int w) {
+    auto tile = [&](const char* Q, int gi, int qi) {
         const char* DO = Q + TILE;
         const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
         const float* DL = LS + 64;
-        const int qt = qlo + (w % ntq) * QT;
-        const int win = (h0 + w / ntq) < a.local_heads ? a.window : -1;
+        const int qt = qlo + qi * QT;
+        const int win = (h0 + gi) < a.local_heads ? a.window : -1;
         uint32_t hs = 0;
-        if constexpr (DROP) hs = drop_head(a.seed, h0 + w / ntq);
+        if constexpr (DROP) hs = drop_head(a.seed, h0 + gi);
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
                                (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
         f32x16 s = f32x16{}, dp = f32x16{};
@@ -224,18 +226,34 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 
     char* buf0 = smem + VIMG;
     char* buf1 = buf0 + BUF;
-    if (nwork > 0) issue(0, buf0);
+    int ig = 0, iq = 0, cg = 0, cq = 0;  // next item to issue / to compute
+    auto adv = [&](int& g, int& q) {
+        if (++q == ntq) {
+            q = 0;
+            ++g;
+        }
+    };
+    if (nwork > 0) {
+        issue(ig, iq, buf0);
+        adv(ig, iq);
+    }
     __syncthreads();
     int w = 0;
     for (; w + 1 < nwork; w += 2) {
-        issue(w + 1, buf1);
-        tile(buf0, w);
+        issue(ig, iq, buf1);
+        adv(ig, iq);
+        tile(buf0, cg, cq);
+        adv(cg, cq);
         __syncthreads();
-        if (w + 2 < nwork) issue(w + 2, buf0);
-        tile(buf1, w + 1);
+        if (w + 2 < nwork) {
+            issue(ig, iq, buf0);
+            adv(ig, iq);
+        }
+        tile(buf1, cg, cq);
+        adv(cg, cq);
         __syncthreads();
     }
-    if (w < nwork) tile(buf0, w);
+    if (w < nwork) tile(buf0, cg, cq);
 
     if (mykey < Lk) {
         if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel

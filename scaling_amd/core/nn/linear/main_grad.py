@@ -185,16 +185,25 @@ class _MultiLinear(torch.autograd.Function):
                 g2 = g2 * col
             target = _main_grad_target(weights)
             if target is not None:
+                # lazily zeroed gradients (optimizer ``lazy_grad_zeroing``): the first write of the step overwrites
+                # (beta = 0) instead of accumulating into a zeroed buffer
+                fresh = [getattr(wt, "_sa_fresh", False) for wt in weights]
+                accumulate = not all(fresh)
+                for wt, f in zip(weights, fresh):
+                    if f:
+                        wt._sa_fresh = False
+                        if accumulate:
+                            wt.grad.zero_()
                 ws = wgrad_stream(g2.device)
                 if ws is not None:
                     ws.wait_stream(torch.cuda.current_stream(g2.device))
                     with torch.cuda.stream(ws):
-                        wgrad(g2, x2, target, accumulate=True)
+                        wgrad(g2, x2, target, accumulate=accumulate)
                     g2.record_stream(ws)  # keep the operands' memory until the side stream is done
                     x2.record_stream(ws)
                     _queue_end_of_backward_sync(g2.device)
                 else:
-                    wgrad(g2, x2, target, accumulate=True)
+                    wgrad(g2, x2, target, accumulate=accumulate)
                 for wt in weights:
                     cb = getattr(wt, "_sa_grad_ready", None)
                     if cb is not None:

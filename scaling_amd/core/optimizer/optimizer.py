@@ -79,6 +79,13 @@ class Optimizer(BaseOptimizer):
         self._zero_event: Optional[Any] = None  # gradient zeroing of the last overlapped step
         self._layer_buckets: dict[int, list[tuple[int, int]]] = {}
         self._hooks = []
+        self._fresh_hooks = []
+        self._lazy_zero = bool(config.lazy_grad_zeroing)
+        if self._lazy_zero:
+            for g in parameter_groups:
+                for p in g.parameters_original:
+                    if p.requires_grad:
+                        self._fresh_hooks.append(p.register_hook(self._make_fresh_hook(p)))
         if self.dp > 1 and config.overlap_grad_reduce and not topology.config.sequence_parallel:
             for gi, g in enumerate(parameter_groups):
                 for pi, p in enumerate(g.parameters_original):
@@ -128,6 +135,23 @@ class Optimizer(BaseOptimizer):
                     self._launch_bucket(gi, b)
 
         return hook
+
+    @staticmethod
+    def _make_fresh_hook(p: torch.Tensor) -> Any:
+        """Runs before autograd accumulates a gradient into ``p.grad``: a lazily zeroed gradient is cleared first."""
+
+        def hook(g: torch.Tensor) -> None:
+            if getattr(p, "_sa_fresh", False):
+                p._sa_fresh = False  # type: ignore[attr-defined]
+                p.grad.zero_()  # type: ignore[union-attr]
+            return None
+
+        return hook
+
+    def materialize_fresh_grads(self) -> None:
+        """Zeroes the lazily zeroed gradients that received nothing this step (before anything reads them)."""
+        for g in self.parameter_groups:
+            g.materialize_fresh()
 
     # ------------------------------------------------------------------ gradient sync
     def _launch_bucket(self, gi: int, b: int) -> None:
@@ -193,9 +217,9 @@ class Optimizer(BaseOptimizer):
                     dist.all_reduce(p.grad, group=self.topology.model_parallel_group)
 
     # ------------------------------------------------------------------ step
-    def zero_grad(self, set_to_none: bool = True) -> None:
+    def zero_grad(self, set_to_none: bool = True, lazy: bool = False) -> None:
         for g in self.parameter_groups:
-            g.zero_grad(set_to_none)
+            g.zero_grad(set_to_none, lazy=lazy and self._lazy_zero)
 
     def backward(self, loss: torch.Tensor) -> None:
         self.wait_grad_zeroing()
@@ -291,6 +315,7 @@ class Optimizer(BaseOptimizer):
     def step(self) -> OptimizerStepOutput:
         self.wait_param_sync()  # parameters never touched by a forward (frozen / unused) still must land
         sync_wgrad_stream(self.topology.device)  # (also done at the end of every backward)
+        self.materialize_fresh_grads()
         self.step_index += 1
         for g in self.parameter_groups:
             g.set_dummy_grad()
@@ -301,7 +326,7 @@ class Optimizer(BaseOptimizer):
         ls_out = self.loss_scaler.step(overflow)
         if self.config.loss_scaler.enable and overflow:
             logger.warning("loss scaler encountered overflow, skipping step")
-            self.zero_grad()
+            self.zero_grad(lazy=True)
             return OptimizerStepOutput(None, None, None, ls_out.overflow, ls_out.no_overflow_steps,
                                        ls_out.current_loss_scale, None)
         if overflow:
@@ -349,7 +374,7 @@ class Optimizer(BaseOptimizer):
                         ev = torch.cuda.Event()
                         ev.record(torch.cuda.current_stream(self.topology.device))
                         self._ag_events[(gi, b)] = ev
-            self.zero_grad()
+            self.zero_grad(lazy=True)
             if overlap:
                 self._zero_event = torch.cuda.Event()
                 self._zero_event.record(torch.cuda.current_stream(self.topology.device))

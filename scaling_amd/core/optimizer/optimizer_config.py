@@ -31,6 +31,12 @@ class OptimizerConfig(BaseConfig):
         description="run the AdamW update (and the ZeRO all-gather) bucket by bucket on a side stream; the next "
         "forward waits per layer for its buckets, the next backward for the gradient zeroing (GPU only)",
     )
+    lazy_grad_zeroing: bool = Field(
+        False,
+        description="defer each parameter's gradient zeroing to its first gradient write of the next step (the "
+        "GEMM-fused weight gradient then writes with beta = 0): no full-buffer memset per step.  Requires that "
+        "gradients are produced only by backward passes (code that writes .grad directly must leave it off)",
+    )
     overlap_param_gather: bool = Field(
         True,
         description="ZeRO: all-gather updated parameters bucket by bucket on a side stream and let each pipeline "

@@ -32,6 +32,16 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def _merge_ranges(rs: list[tuple[int, int]]) -> list[tuple[int, int]]:
+    out: list[tuple[int, int]] = []
+    for a, b in sorted(rs):
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
+
+
 class OptimizerParamGroup:
     def __init__(self, named_parameters_with_meta: list[tuple[str, torch.Tensor, CoreParameterMeta]],
                  config: OptimizerParamGroupConfig):
@@ -100,6 +110,17 @@ class OptimizerParamGroup:
             rng for i, m in enumerate(self.parameter_metas) if m.is_model_parallel_duplicate
             for rng in self.owned_ranges(i)
         ]
+        # lazy gradient zeroing: tied / TP-constant-tied grads are read by cross-rank reductions before any
+        # optimizer hook could materialise them, so they are zeroed eagerly; every other parameter's zeroing is
+        # deferred to its first gradient write of the step (see ``zero_grad``)
+        self._eager_ranges = _merge_ranges([
+            (o, o + n) for (o, n), m in zip(self.param_offsets, self.parameter_metas)
+            if m.is_tied or m.tied_grad_on_model_parallel
+        ])
+        self._lazy_params = [
+            p for p, m in zip(self.parameters_original, self.parameter_metas)
+            if not (m.is_tied or m.tied_grad_on_model_parallel)
+        ]
         # param -> buckets, bucket -> number of params overlapping it
         self.param_buckets: list[list[int]] = []
         self.bucket_param_count = [0] * B
@@ -154,9 +175,32 @@ class OptimizerParamGroup:
             for b, s in enumerate(self.owned_flat_starts):
                 self.owned_view(self.master, b).copy_(self.flat_param[s : s + self.chunk])
 
-    def zero_grad(self, set_to_none: bool = True) -> None:
-        self.flat_grad.zero_()
+    def zero_grad(self, set_to_none: bool = True, lazy: bool = False) -> None:
+        """Zeroes the flat gradient buffer.
+
+        ``lazy``: only the eagerly zeroed ranges are cleared now; every other parameter is marked ``_sa_fresh``
+        and its stale gradient is never read: the GEMM-fused weight-gradient path writes it with beta = 0
+        (``core/nn/linear/main_grad.py``), the optimizer's tensor hook zeroes it right before autograd
+        accumulates into it, and ``materialize_fresh`` zeroes whatever received no gradient at all before the
+        step reads the buffer.  Saves one full write of the gradient buffer per step and the beta = 1 read
+        of zeros in every first weight-gradient GEMM."""
+        if not lazy:
+            self.flat_grad.zero_()
+            for p in self.parameters_original:
+                p._sa_fresh = False  # type: ignore[attr-defined]
+        else:
+            for a, b in self._eager_ranges:
+                self.flat_grad[a:b].zero_()
+            for p in self._lazy_params:
+                p._sa_fresh = True  # type: ignore[attr-defined]
         self.attach_grads()
+
+    def materialize_fresh(self) -> None:
+        """Zeroes the gradients of parameters that are still ``_sa_fresh`` (no gradient written this step)."""
+        for p in self._lazy_params:
+            if getattr(p, "_sa_fresh", False):
+                p._sa_fresh = False  # type: ignore[attr-defined]
+                p.grad.zero_()  # type: ignore[union-attr]
 
     def log_state(self) -> None:
         pass

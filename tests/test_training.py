@@ -90,3 +90,26 @@ def test_train_and_resume_bit_exact(tmp_path, mp, pp, world, extra):
     assert (tmp_path / "ckpt" / "global_step6").is_dir()
     # the profiler wrote its timings
     assert any(p.name == "profile.json" for p in (tmp_path / "logs").rglob("profile.json"))
+
+
+@pytest.mark.parametrize(
+    "mp,pp,world,extra",
+    [
+        (1, 1, 2, {}),
+        (2, 1, 2, {}),
+        (1, 2, 2, {"weight_tying": True}),
+    ],
+)
+def test_lazy_grad_zeroing_matches_eager(tmp_path, mp, pp, world, extra):
+    """Optimizer ``lazy_grad_zeroing`` (no per-step gradient memset; first GEMM-fused weight-gradient write with
+    beta = 0, autograd-accumulated grads zeroed by a tensor hook, untouched grads zeroed before the step) must give
+    bit-identical losses to eager zeroing, with gradient accumulation, ZeRO, TP and tied weights under PP."""
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, mp, pp, world, **extra)
+    cfg["trainer"]["save_dir"] = None
+    cfg["trainer"]["load_dir"] = None
+    eager = _run(tmp_path, cfg, world, "eager")
+    cfg["optimizer"]["lazy_grad_zeroing"] = True
+    lazy = _run(tmp_path, cfg, world, "lazy")
+    assert [m["training/loss"] for m in lazy] == [m["training/loss"] for m in eager]
+    assert [m["training/global_grad_norm"] for m in lazy] == [m["training/global_grad_norm"] for m in eager]
