@@ -36,6 +36,9 @@ from typing import Any, Optional
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "tokens/sec (whole node) Llama-2-7B-shape bf16, TP×PP×DP on 1/2/4/8 MI355X"
+# the unmodified reference on one MI355X, same shape / batch / protocol (BASELINE.md "Measured same-hardware
+# reference point", tools/reference_bench/ref_bench.py): the reference publishes no number of its own
+REFERENCE_TOK_S_1GPU = 9909.0
 
 
 def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
@@ -316,7 +319,9 @@ def _worker(a: argparse.Namespace) -> None:
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": (tokens / sec) / (REFERENCE_TOK_S_1GPU * world) if headline and not a.lora else None,
+            "baseline": "unmodified reference on MI355X (torch attention, best micro-batch 2 x acc 4): "
+                        f"{REFERENCE_TOK_S_1GPU:.0f} tok/s per GPU x n_gpus (BASELINE.md)",
             "dtype": "bf16" if a.precision == "bfloat16" else "fp32",
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
