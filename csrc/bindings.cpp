@@ -310,6 +310,34 @@ at::Tensor transpose2d(const at::Tensor& x) {
     return out;
 }
 
+// ------------------------------------------------------------------ GEMV (decode-time linear layers)
+// y[M, N] = x[M, K] W[N, K]^T (+ b), M <= 4, bf16 / fp16, unit inner strides, 16-B aligned rows
+bool gemv_ok(const at::Tensor& x, const at::Tensor& W) {
+    if (!(x.is_cuda() && W.is_cuda() && x.dim() == 2 && W.dim() == 2)) return false;
+    if (x.scalar_type() != W.scalar_type() || (x.scalar_type() != at::kBFloat16 && x.scalar_type() != at::kHalf))
+        return false;
+    if (x.size(0) < 1 || x.size(0) > 4 || x.size(1) != W.size(1) || x.size(1) % 8 != 0 || W.size(0) < 1) return false;
+    if (x.stride(1) != 1 || W.stride(1) != 1 || (x.size(0) > 1 && x.stride(0) % 8 != 0) || W.stride(0) % 8 != 0)
+        return false;
+    return (uintptr_t)x.data_ptr() % 16 == 0 && (uintptr_t)W.data_ptr() % 16 == 0;
+}
+at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, c10::optional<at::Tensor> bias) {
+    TORCH_CHECK(gemv_ok(x, W), "gemv: unsupported operands (x [M<=4, K], W [N, K], bf16/fp16, K % 8 == 0, aligned)");
+    const at::DeviceGuard g(x.device());
+    const int64_t M = x.size(0), N = W.size(0), K = W.size(1);
+    const void* bp = nullptr;
+    at::Tensor bc;
+    if (bias.has_value() && bias->defined()) {
+        TORCH_CHECK(bias->numel() == N && bias->scalar_type() == W.scalar_type(), "gemv: bias");
+        bc = bias->contiguous();
+        bp = bc.data_ptr();
+    }
+    auto y = at::empty({M, N}, x.options());
+    sa_launch::gemv(dt(x), (int)M, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), bp, y.data_ptr(), N, (int)N,
+                    (int)K, cur_stream());
+    return y;
+}
+
 // ------------------------------------------------------------------ GEMM (weight gradient)
 // C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
 bool gemm_tn_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
@@ -553,6 +581,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("ar_allreduce", &ar_allreduce, "one-shot all-reduce of x over the registered buffers (in place)");
     m.def("transpose_ok", &transpose_ok, "whether transpose2d supports this tensor");
     m.def("transpose2d", &transpose2d, "x^T (contiguous) for 2-byte 2-D matrices");
+    m.def("gemv_ok", &gemv_ok, "whether gemv supports these operands");
+    m.def("gemv", &gemv, "y = x W^T (+ b) for at most 4 rows of x (decode-time linear layers)", py::arg("x"), py::arg("W"), py::arg("bias") = py::none());
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
     m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());

@@ -133,3 +133,9 @@ namespace sa_launch {
 void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64_t slot_off, int64_t flag_off,
                        uint32_t epoch, bool signal, void* out, int64_t n, int* err, hipStream_t st);
 }
+
+namespace sa_launch {
+// gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ b) for M <= 4 (decode-time linear layers), bf16 / fp16, K % 8 == 0
+void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, void* y, int64_t ldy,
+          int N, int K, hipStream_t st);
+}  // namespace sa_launch

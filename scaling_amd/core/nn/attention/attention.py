@@ -162,6 +162,49 @@ class KVCache:
         return self.k[: self.length], self.v[: self.length]
 
 
+class DecodeState:
+    """Device-resident position of a graph-captured decode loop, shared by every layer's ``StaticKVCache``:
+    ``pos`` [1] int64 is the position (= cache row) of the token being fed, ``cu_k`` [2] int32 = [0, pos + 1] the
+    key range the flash-decoding kernel reads.  ``advance`` moves both on the device (inside the graph)."""
+
+    def __init__(self, n_prompt: int, device: torch.device) -> None:
+        self.pos = torch.full((1,), n_prompt, dtype=torch.long, device=device)
+        self.cu_k = torch.tensor([0, n_prompt + 1], dtype=torch.int32, device=device)
+
+    def reset(self, n_prompt: int) -> None:
+        self.pos.fill_(n_prompt)
+        self.cu_k[1:].fill_(n_prompt + 1)
+
+    def advance(self) -> None:
+        self.pos.add_(1)
+        self.cu_k[1:].add_(1)
+
+
+class StaticKVCache:
+    """Fixed-capacity decode cache for HIP-graph capture: the new token's K/V rows are written at the device-side
+    position (``index_copy_``) and attention reads the whole buffer with a device-side key range, so one decode
+    step has the same shapes, pointers and launches at every position (``KVCache`` grows on the host instead)."""
+
+    def __init__(self, k: torch.Tensor, v: torch.Tensor, state: DecodeState) -> None:
+        self.k, self.v, self.state = k, v, state
+
+    @classmethod
+    def from_cache(cls, kv: "KVCache", capacity: int, state: DecodeState) -> "StaticKVCache":
+        n = kv.length
+        assert capacity >= n, (capacity, n)
+        kb = kv.k.new_zeros((capacity,) + tuple(kv.k.shape[1:]))
+        vb = kv.v.new_zeros((capacity,) + tuple(kv.v.shape[1:]))
+        kb[:n].copy_(kv.k[:n])
+        vb[:n].copy_(kv.v[:n])
+        return cls(kb, vb, state)
+
+    def append(self, k: torch.Tensor, v: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        assert k.shape[0] == 1, "graph-captured decoding feeds one token per step"
+        self.k.index_copy_(0, self.state.pos, k)
+        self.v.index_copy_(0, self.state.pos, v)
+        return self.k, self.v, self.state.cu_k
+
+
 class ParallelSelfAttention(torch.nn.Module):
     def __init__(
         self,
@@ -375,13 +418,17 @@ class ParallelSelfAttention(torch.nn.Module):
             if not self.causal:
                 raise ValueError("KV caching is only supported for causal attention.")
             assert b == 1, f"KV caching is only supported for batch size 1, got {b}"
-            if reset_cache:
-                self.cache[cache_index] = KVCache.start(k, v)
+            kv = None if reset_cache else self.cache[cache_index]
+            if isinstance(kv, StaticKVCache):  # graph-captured decoding: device-side write index and key range
+                assert self.use_flash_attention, "graph-captured decoding needs the flash attention kernel"
+                k, v, cumulative_seq_lengths_key = kv.append(k, v)
             else:
-                kv = self.cache[cache_index]
-                assert isinstance(kv, KVCache), "use_cache without a preceding reset_cache"
-                k, v = kv.append(k, v)
-            cumulative_seq_lengths_key = torch.tensor([0, k.shape[0]], device=x.device, dtype=torch.int32)
+                if reset_cache:
+                    self.cache[cache_index] = KVCache.start(k, v)
+                else:
+                    assert isinstance(kv, KVCache), "use_cache without a preceding reset_cache"
+                    k, v = kv.append(k, v)
+                cumulative_seq_lengths_key = torch.tensor([0, k.shape[0]], device=x.device, dtype=torch.int32)
         elif reset_cache:
             self.cache[cache_index] = (None, None)
 

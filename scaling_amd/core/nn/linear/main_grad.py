@@ -49,6 +49,7 @@ from typing import Any, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ....ops.gemm import linear as gemm_linear
 from ....ops.gemm import transpose2d, wgrad
 
 _GEN = [0]
@@ -136,6 +137,24 @@ def _adjacent(ts: Sequence[Optional[torch.Tensor]]) -> Optional[torch.Tensor]:
     return torch.as_strided(first, (rows, K), (K, 1))
 
 
+def _rehome_adjacent(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Moves weights that no optimizer flat buffer owns (inference, frozen base weights) into one contiguous
+    buffer, once, so the fused GEMM reads a zero-copy ``[sum N, K]`` view instead of concatenating every call
+    (``torch.cat`` of the q/k/v or gate/up weights per forward costs more than the GEMV it feeds)."""
+    if any(getattr(w, "_sa_main_grad", False) for w in weights):
+        return None
+    if len({(w.dtype, w.device, w.shape[-1]) for w in weights}) != 1 or any(w.dim() != 2 for w in weights):
+        return None
+    with torch.no_grad():
+        buf = torch.cat([w.detach() for w in weights], dim=0)
+        off = 0
+        for w in weights:
+            n = w.shape[0]
+            w.data = buf[off : off + n]
+            off += n
+    return _adjacent(weights)
+
+
 def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
     if not all(getattr(w, "_sa_main_grad", False) and w.grad is not None for w in weights):
         return None
@@ -155,7 +174,7 @@ class _MultiLinear(torch.autograd.Function):
         b = None
         if has_bias:
             b = biases[0] if n == 1 else torch.cat(biases, dim=0)  # type: ignore[arg-type]
-        out = torch.nn.functional.linear(x, w, b)
+        out = gemm_linear(x, w, b)
         wt = _transposed(weights, w) if want_wt else None
         ctx.has_wt = wt is not None
         ctx.save_for_backward(x, wt if wt is not None else w, *weights)
@@ -233,6 +252,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 def multi_linear(x: torch.Tensor, weights: Sequence[torch.Tensor], biases: Optional[Sequence[Optional[torch.Tensor]]] = None,
                  tp_group: Any = None) -> torch.Tensor:
     """``x @ [W_1; ...; W_n]^T (+ [b_1; ...; b_n])`` as one GEMM (forward, dgrad and wgrad)."""
+    if len(weights) > 1 and _adjacent(weights) is None:
+        _rehome_adjacent(weights)
     want_wt = torch.is_grad_enabled() and x.requires_grad
     if biases is None or any(b is None for b in biases):
         return _MultiLinear.apply(x, len(weights), want_wt, tp_group, *weights)

@@ -5,6 +5,9 @@ kernel stages them as they lie (LDS-DMA) and builds MFMA fragments with the tran
 ping-pong schedule.  At the 7B layer shapes it runs 1.05-1.25 PF vs hipBLASLt's 0.95-1.2 PF
 (``profiles/gemm_wgrad_r1.log``).  Shapes it does not tile (M/N not multiples of 256, T not a multiple
 of 64) use ``torch.matmul`` / ``addmm_`` (hipBLASLt).
+
+``linear`` is the forward ``x W^T (+ b)`` of every linear layer: at most 4 token rows (token-by-token decoding)
+run the weight-streaming GEMV kernel (``csrc/kernels/gemv.hip``), everything else hipBLASLt.
 """
 from __future__ import annotations
 
@@ -34,3 +37,17 @@ def transpose2d(x: torch.Tensor) -> torch.Tensor:
     if use_native(x) and ext().transpose_ok(x):
         return ext().transpose2d(x)
     return x.t().contiguous()
+
+
+GEMV_MAX_ROWS = 4
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear(x, w, b)``; decode-sized inputs (<= 4 rows) on the GEMV kernel."""
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    if 0 < rows <= GEMV_MAX_ROWS and use_native(x) and w.dim() == 2:
+        x2 = x.reshape(rows, K)
+        if ext().gemv_ok(x2, w) and (b is None or b.dtype == w.dtype):
+            return ext().gemv(x2, w, b).reshape(*x.shape[:-1], w.shape[0])
+    return torch.nn.functional.linear(x, w, b)

@@ -91,15 +91,24 @@ class TransformerInferenceModule(InferenceModule):
 
     def generate(self, max_tokens: int, input_text: Optional[str] = None, input_tokens: Optional[list[int]] = None,
                  sample_fn: Callable[[torch.Tensor], torch.Tensor] = sample_argmax,
-                 stop_tokens: Optional[Sequence[int]] = None, use_cache: bool = True) -> CompletionOutput:
+                 stop_tokens: Optional[Sequence[int]] = None, use_cache: bool = True,
+                 use_cuda_graph: bool = False) -> CompletionOutput:
         """Completion text / tokens / logits for a prompt.  With the KV cache each step feeds only the new
-        token (with its absolute position); without it the whole sequence is re-run."""
+        token (with its absolute position); without it the whole sequence is re-run.
+
+        ``use_cuda_graph`` (KV cache, one GPU, flash attention, a graph-safe sampler such as ``sample_argmax``):
+        after the prefill, the decode step is captured once as a HIP graph and replayed per token
+        (``graph_decode.GraphDecoder``) — same kernels and results as the eager loop, without its per-token
+        launch and Python overhead."""
         if stop_tokens is None:
             assert self.tokenizer is not None, "If no tokenizer is provided, a stop token needs to be set manually"
             stop_tokens = [self.tokenizer.eos_token_id]
         cur = self._pre_process_input(input_text, input_tokens, process_for_cached_inference=use_cache)
         assert cur.input_token_ids is not None
         n_in = cur.input_token_ids.shape[-1]
+        if use_cuda_graph:
+            assert use_cache, "graph-captured decoding needs the KV cache"
+            return self._generate_graph(cur, n_in, max_tokens, sample_fn, stop_tokens)
         settings = InferenceSettings(use_cache=use_cache, reset_cache=not use_cache, cache_index=0, embedding_layers=[-1])
         tokens: list[int] = []
         step_logits: list[torch.Tensor] = []
@@ -123,5 +132,19 @@ class TransformerInferenceModule(InferenceModule):
         else:
             assert out is not None
             logits = self._post_process_output(out)[n_in - 1 :]
+        text = self.tokenizer.decode(tokens) if self.tokenizer is not None else None
+        return CompletionOutput(completion_text=text, completion_tokens=tokens, completion_logits=logits)
+
+    def _generate_graph(self, prompt: TextDatasetBatch, n_in: int, max_tokens: int,
+                        sample_fn: Callable[[torch.Tensor], torch.Tensor], stop_tokens: Sequence[int]) -> CompletionOutput:
+        from .graph_decode import GraphDecoder
+
+        assert self.devices is not None and len(self.devices) == 1, "graph-captured decoding runs on one device"
+        out = self.forward(prompt)  # prefill (reset_cache): fills each layer's KVCache
+        first = sample_fn(out.activations)
+        assert first.is_cuda, "graph-captured decoding needs a GPU"
+        dec = GraphDecoder(self, n_in, max_tokens, first, sample_fn, out.activations[:, -1, :])
+        dec.capture()
+        tokens, logits = dec.run(stop_tokens)
         text = self.tokenizer.decode(tokens) if self.tokenizer is not None else None
         return CompletionOutput(completion_text=text, completion_tokens=tokens, completion_logits=logits)

@@ -12,6 +12,7 @@ import torch
 
 from ....core import ColumnParallelLinear, Topology, VocabParallelEmbedding
 from ....core.nn.linear.utils import all_concat, copy_to_tensor_model_parallel_region
+from ....ops.gemm import linear as gemm_linear
 from ...context.config import TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
 from .embedding import _device
@@ -72,4 +73,4 @@ class TransformerLMHeadTied(TransformerLayerBaseIO):
         act = x.activations
         if self.topology is not None and self.topology.config.model_parallel_size > 1:
             act = copy_to_tensor_model_parallel_region(act, topology=self.topology)
-        return _finish(self, x, torch.nn.functional.linear(act, self.embedding.weight), self.vocab_per_rank)
+        return _finish(self, x, gemm_linear(act, self.embedding.weight), self.vocab_per_rank)

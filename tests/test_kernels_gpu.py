@@ -658,3 +658,34 @@ def test_flash_decoding_forward_with_prefill_backward():
     """Tiny training segments (max_q x group <= 32) run the decode forward and the regular backward kernels."""
     _attn_case([7, 5], 4, 1, 64, True)
     _attn_case([8], 4, 4, 128, False)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (1, 22016, 4096), (1, 4096, 11008), (2, 1003, 200), (3, 77, 64),
+                                   (4, 32000, 4096), (1, 5, 8)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemv(dtype, M, N, K, bias):
+    """Decode-time linear layer y = x W^T (+ b) for <= 4 rows against an fp32 reference, through ops.gemm.linear
+    (which must route these shapes to the GEMV kernel)."""
+    from scaling_amd.ops import gemm
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=dtype)
+    w = torch.randn(N, K, device=DEV, dtype=dtype) / math.sqrt(K)
+    b = torch.randn(N, device=DEV, dtype=dtype) if bias else None
+    assert ext().gemv_ok(x, w)
+    y = gemm.linear(x.view(M, 1, K), w, b).view(M, N)
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    # the same through a row-strided view of a wider weight (fused q/k/v / gate-up buffers)
+    wide = torch.randn(N, K + 64, device=DEV, dtype=dtype) / math.sqrt(K)
+    wv = wide[:, 32 : 32 + K]
+    torch.testing.assert_close(ext().gemv(x, wv).float(), x.float() @ wv.float().t(), atol=2e-2, rtol=2e-2)
+
+
+def test_gemv_rejects_unsupported():
+    x = torch.randn(5, 64, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(32, 64, device=DEV, dtype=torch.bfloat16)
+    assert not ext().gemv_ok(x, w)  # more than 4 rows: hipBLASLt
+    assert not ext().gemv_ok(x[:1, :60], w[:, :60])  # K % 8
+    assert not ext().gemv_ok(x[:1].float(), w.float())  # fp32
