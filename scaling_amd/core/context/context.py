@@ -16,6 +16,7 @@ import torch.distributed as dist
 
 from ..config import BaseConfig
 from ..topology import Topology, TopologyState
+from ..utils.checkpoint_writer import save_file
 from ..utils.safe_load import safe_load
 
 
@@ -95,7 +96,7 @@ class BaseContext:
         dir = Path(dir)
         if self.topology.config.global_rank == 0:
             self.config.save(dir / "config.yml")
-        torch.save(self.state_dict(), str(dir / f"context_global_rank_{self.topology.config.global_rank}.pt"))
+        save_file(self.state_dict(), str(dir / f"context_global_rank_{self.topology.config.global_rank}.pt"))
 
     def load_checkpoint(self, dir: Path | str) -> None:
         dir = Path(dir)

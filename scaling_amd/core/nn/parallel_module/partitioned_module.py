@@ -16,6 +16,7 @@ import torch
 
 from ...logging import logger
 from ...topology import PipePartitionMethod
+from ...utils.checkpoint_writer import save_file
 from ...utils.param_merge import merge_parameter, split_parameter
 from ..linear.main_grad import invalidate_transposed_weights
 from ..parameter_meta import CoreParameterMeta
@@ -147,7 +148,7 @@ class PipePartitionedModule(torch.nn.Module):
                     if not sd:
                         continue
                     fname = f"model_state_layer_{li}_{layer.__class__.__name__}{'' if sep == '' else '_'}{sep}.pt"
-                    torch.save(sd, str(dir_ / fname))
+                    save_file(sd, dir_ / fname)
 
     def load_checkpoint(
         self,

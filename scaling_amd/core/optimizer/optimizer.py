@@ -40,6 +40,7 @@ from ..logging import logger
 from ..nn.linear.main_grad import invalidate_transposed_weights, sync_wgrad_stream, wgrad_stream
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
+from ..utils.checkpoint_writer import save_file
 from ..utils.safe_load import safe_load
 from .base import BaseOptimizer, OptimizerStepOutput
 from .loss_scaler import LossScaler
@@ -47,6 +48,12 @@ from .optimizer_config import OptimizerConfig
 from .parameter_group import OptimizerParamGroup
 
 _SLOTS = ("exp_avg", "exp_avg_sq")
+
+
+def _is_sp_norm_param(name: str) -> bool:
+    """Norm parameters see only their sequence shard under sequence parallelism: their gradients are summed
+    over the TP group before the DP reduction (reference ``optimizer.py:253-260`` selects them by name)."""
+    return "norm" in name
 
 
 class Optimizer(BaseOptimizer):
@@ -86,7 +93,7 @@ class Optimizer(BaseOptimizer):
                 for p in g.parameters_original:
                     if p.requires_grad:
                         self._fresh_hooks.append(p.register_hook(self._make_fresh_hook(p)))
-        if self.dp > 1 and config.overlap_grad_reduce and not topology.config.sequence_parallel:
+        if self.dp > 1 and config.overlap_grad_reduce:
             for gi, g in enumerate(parameter_groups):
                 for pi, p in enumerate(g.parameters_original):
                     if p.requires_grad and hasattr(p, "register_post_accumulate_grad_hook"):
@@ -106,12 +113,15 @@ class Optimizer(BaseOptimizer):
         assert not dups, f"parameters occurring more than once: {dups}"
 
     def _deferred_buckets(self) -> list[set[int]]:
-        """Buckets that must wait for ReduceTiedGrads / TP-constant grads before the DP reduction."""
+        """Buckets that must wait for ReduceTiedGrads / TP-constant grads (and, under sequence parallelism, the
+        TP all-reduce of the norm weights' partial gradients) before the DP reduction; every other bucket is
+        reduced as soon as its gradients are final, overlapped with the rest of the backward."""
+        sp = self.topology.config.sequence_parallel and self.topology.config.model_parallel_size > 1
         out = []
         for g in self.parameter_groups:
             s: set[int] = set()
-            for m, bs in zip(g.parameter_metas, g.param_buckets):
-                if m.is_tied or m.tied_grad_on_model_parallel:
+            for n, m, bs in zip(g.parameter_names, g.parameter_metas, g.param_buckets):
+                if m.is_tied or m.tied_grad_on_model_parallel or (sp and _is_sp_norm_param(n)):
                     s.update(bs)
             out.append(s)
         return out
@@ -213,7 +223,7 @@ class Optimizer(BaseOptimizer):
             return
         for g in self.parameter_groups:
             for n, p in zip(g.parameter_names, g.parameters_original):
-                if "norm" in n and p.grad is not None:
+                if _is_sp_norm_param(n) and p.grad is not None:
                     dist.all_reduce(p.grad, group=self.topology.model_parallel_group)
 
     # ------------------------------------------------------------------ step
@@ -472,7 +482,7 @@ class Optimizer(BaseOptimizer):
         topo = self.topology
         if self.config.zero and self.config.zero_save_static:
             sd = self.state_dict()
-            torch.save(sd, str(directory / f"optimizer_state_static_mp_{topo.model_parallel_rank}_pp_{topo.pipe_parallel_rank}_dp_{topo.data_parallel_rank}.pt"))
+            save_file(sd, str(directory / f"optimizer_state_static_mp_{topo.model_parallel_rank}_pp_{topo.pipe_parallel_rank}_dp_{topo.data_parallel_rank}.pt"))
             return
         if topo.data_parallel_rank != 0 and not self.config.zero:
             return
@@ -502,7 +512,7 @@ class Optimizer(BaseOptimizer):
                     d["parameters"][m2.key_for_layer(meta.layer_index)] = entry
         if topo.model_parallel_rank == 0 and topo.data_parallel_rank == 0:
             for li, d in by_layer.items():
-                torch.save(d, str(directory / f"optimizer_state_layer_{li}.pt"))
+                save_file(d, str(directory / f"optimizer_state_layer_{li}.pt"))
         logger.info("saved optimizer checkpoint")
 
     def load_checkpoint(self, directory: Union[Path, str]) -> None:

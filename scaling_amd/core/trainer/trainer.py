@@ -12,6 +12,7 @@ from typing import Any, Callable, Generic, Optional, TypeVar
 
 import torch
 
+from ..utils.checkpoint_writer import checkpoint_writer
 from ..utils.watchdog import HangWatchdog
 from ..context import BaseContext, DeterminedBaseContext
 from ..data import BaseDataset, DataLoader
@@ -40,6 +41,8 @@ class BaseTrainer(Generic[BaseContextGeneric, ParallelModuleGeneric]):
         self.config = config
         self.context = context
         self.parallel_module = parallel_module
+        self._unpublished: Optional[tuple[Path, int]] = None  # async checkpoint written but not yet 'latest'
+        checkpoint_writer.configure(config.async_checkpointing)
         self.parameters_total, self.parameters_unique = parallel_module.get_params_count()
         logger.log_config_dict({"parameters_total": self.parameters_total, "parameters_unique": self.parameters_unique})
         logger.info(f"parameters total {self.parameters_total} unique {self.parameters_unique}")
@@ -82,6 +85,10 @@ class BaseTrainer(Generic[BaseContextGeneric, ParallelModuleGeneric]):
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, save_dir: Optional[Path] = None) -> Path:
+        """Writes ``global_step<N>/`` and points ``latest`` at it.  With ``async_checkpointing`` the files are
+        written by a background thread and ``latest`` moves at the next ``flush_checkpoints`` (next save or end
+        of training), once every rank's files are complete."""
+        self.flush_checkpoints()
         save_dir = Path(save_dir or self.config.save_dir)  # type: ignore[arg-type]
         it_dir = save_dir / f"global_step{self.context.iterations}"
         it_dir.mkdir(exist_ok=True, parents=True)
@@ -90,13 +97,35 @@ class BaseTrainer(Generic[BaseContextGeneric, ParallelModuleGeneric]):
         self.parallel_module.save_checkpoint(it_dir, separate_file_for_parameters=self.config.separate_file_for_parameters)
         self.optimizer.save_checkpoint(it_dir)
         self.context.save_checkpoint(it_dir)
+        if checkpoint_writer.async_mode:
+            self._unpublished = (save_dir, self.context.iterations)
+            logger.info(f"checkpoint {it_dir} queued for writing")
+            return save_dir
         if torch.distributed.is_initialized():
             torch.distributed.barrier()
-        if self.context.topology.config.global_rank == 0:
-            with open(save_dir / "latest", "w", encoding="UTF-8") as f:
-                f.write(f"global_step{self.context.iterations}")
+        self._publish(save_dir, self.context.iterations)
         logger.info(f"saved checkpoint: {it_dir}")
         return save_dir
+
+    def _publish(self, save_dir: Path, iterations: int) -> None:
+        if self.context.topology.config.global_rank == 0:
+            tmp = save_dir / "latest.tmp"
+            with open(tmp, "w", encoding="UTF-8") as f:
+                f.write(f"global_step{iterations}")
+            os.replace(tmp, save_dir / "latest")
+
+    def flush_checkpoints(self) -> None:
+        """Waits for this rank's queued checkpoint files, then (all ranks) publishes the checkpoint as ``latest``."""
+        if self._unpublished is None:
+            checkpoint_writer.wait()
+            return
+        save_dir, iterations = self._unpublished
+        self._unpublished = None
+        checkpoint_writer.wait()
+        if torch.distributed.is_initialized():
+            torch.distributed.barrier()
+        self._publish(save_dir, iterations)
+        logger.info(f"saved checkpoint: {save_dir / f'global_step{iterations}'}")
 
     def load_checkpoint(
         self,
@@ -209,6 +238,7 @@ class BaseTrainer(Generic[BaseContextGeneric, ParallelModuleGeneric]):
                         out.append(m)
                 if watchdog is not None:
                     watchdog.heartbeat()
+            self.flush_checkpoints()
         finally:
             if watchdog is not None:
                 watchdog.stop()
@@ -279,11 +309,13 @@ class DeterminedBaseTrainer(BaseTrainer[DeterminedBaseContextGeneric, ParallelMo
                 ctx.distributed.broadcast(str(p))
                 path = Path(p)
                 super().save_checkpoint(save_dir=path)
+                self.flush_checkpoints()  # the storage context uploads on exit: files must be complete
             if self.config.delete_past_optimizer_states:
                 self.delete_previous_optimizer_states_determined(str(storage_id))
         else:
             path = Path(ctx.distributed.broadcast(None))
             super().save_checkpoint(save_dir=path)
+            self.flush_checkpoints()
         return path
 
     def load_checkpoint(self, load_dir: Optional[Path] = None, load_optimizer_states: bool = True,

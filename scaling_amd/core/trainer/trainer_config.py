@@ -27,6 +27,11 @@ class TrainerConfig(BaseConfig):
     dataloader_prefetch_factor: Optional[int] = Field(None, description="")
     eval_iterations: int = Field(1, description="(not implemented in the reference either: one eval step)")
     eval_interval: Optional[int] = Field(None, description="evaluate every eval_interval steps")
+    async_checkpointing: bool = Field(
+        False,
+        description="write checkpoint files from a background thread (state snapshotted to host memory first); "
+        "'latest' is updated once every rank's files are complete, at the next save or the end of training",
+    )
     hang_watchdog_seconds: Optional[float] = Field(
         None, description="MI355X addition: dump all thread stacks when a train step makes no progress for this many "
         "seconds (RCCL hang / stuck kernel diagnosis); None disables"
