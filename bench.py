@@ -19,7 +19,9 @@ Rank 0 prints one JSON line; ``value`` is the whole-job tokens/s (global tokens 
 The line also carries what the ranks saw: the world size of the process group, every rank's step time,
 and whether the parameters of all data-parallel replicas agree bit-for-bit after the last step.
 
-``--backend gloo`` runs the same path on CPU processes (plumbing mode for the CPU test-suite).
+``--backend gloo`` runs the same path on CPU processes (plumbing mode for the CPU test-suite);
+``--backend gloo-gpu`` runs GPU ranks (several may share one GPU, which RCCL refuses) with gloo collectives
+standing in for RCCL: a multi-rank rehearsal of the GPU-side paths (streams, events, kernels) on a 1-GPU box.
 """
 from __future__ import annotations
 
@@ -68,8 +70,9 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--lora", action="store_true",
                    help="LoRA finetune path (BASELINE #5): q/k/v/dense adapters trained, base weights frozen")
     p.add_argument("--lora-rank", type=int, default=64)
-    p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo"],
-                   help="gloo = CPU processes (plumbing mode, no GPU)")
+    p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo", "gloo-gpu"],
+                   help="gloo = CPU processes (plumbing mode, no GPU); gloo-gpu = rehearsal: GPU ranks (several "
+                        "may share one GPU) with gloo collectives standing in for RCCL")
     p.add_argument("--precision", type=str, default="bfloat16", choices=["bfloat16", "float32"])
     p.add_argument("--num-layers", type=int, default=None, help="debug only: marks the result as not the headline config")
     p.add_argument("--gemm-tuning", type=str, default="use", choices=["use", "tune", "off"],
@@ -186,8 +189,9 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
         "micro_batch_size": a.micro_batch, "gradient_accumulation_steps": a.grad_acc,
         "activation_checkpointing_type": a.activation_checkpointing, "sequence_parallel": a.sequence_parallel,
     }
-    if a.backend == "gloo":
+    if a.backend in ("gloo", "gloo-gpu"):
         topo["backend"] = "gloo"
+        topo["gloo_on_gpu"] = a.backend == "gloo-gpu"
     return {
         "topology": topo,
         "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero),
@@ -301,7 +305,7 @@ def _worker(a: argparse.Namespace) -> None:
     tokens = gbs * a.seq_len * a.steps
     ms = 1000.0 * sec / a.steps
     if rank == 0:
-        headline = (a.num_layers is None and a.model == "llama2_7b" and a.seq_len == 4096 and gpu
+        headline = (a.num_layers is None and a.model == "llama2_7b" and a.seq_len == 4096 and a.backend == "auto"
                     and a.precision == "bfloat16")
         flops_tok = 6 * unique_params + 12 * arch["num_layers"] * arch["hidden_size"] * a.seq_len
         if a.lora:  # frozen base: no weight-gradient GEMMs for the base weights (~1/3 of the 6N)

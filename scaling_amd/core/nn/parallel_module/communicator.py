@@ -98,6 +98,26 @@ def _bytes_tensor(b: bytes, device: torch.device) -> torch.Tensor:
     return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(device)
 
 
+class _HostStagedWork:
+    """p2p of GPU tensors over gloo (the 1-GPU rehearsal mode, ``TopologyConfig.gloo_on_gpu``): gloo moves raw
+    pointers without ordering against the producing HIP stream, so payloads travel through host copies (the
+    D2H copy of a send is stream-ordered and synchronous; a receive lands in host memory and is copied to the
+    device on the current stream once the transfer finished).  RCCL needs none of this: its p2p is
+    stream-ordered."""
+
+    def __init__(self, works: list[Any], copies: list[tuple[torch.Tensor, torch.Tensor]]) -> None:
+        self.works = works
+        self.copies = copies
+
+    def wait(self) -> bool:
+        for w in self.works:
+            w.wait()
+        for dev_t, host_t in self.copies:
+            dev_t.copy_(host_t)
+        self.works, self.copies = [], []
+        return True
+
+
 class PipeCommunicator:
     max_pending_sends = 8
 
@@ -131,14 +151,23 @@ class PipeCommunicator:
         self._objects = objects
         self._grad_buffers = None
 
+    @property
+    def _host_staged(self) -> bool:
+        return self.local_device.type == "cuda" and dist.get_backend() == "gloo"
+
+    @property
+    def _wire_device(self) -> torch.device:
+        """Device of the (rare) metadata messages: host memory when gloo carries them."""
+        return torch.device("cpu") if self._host_staged else self.local_device
+
     def _send_bytes(self, b: bytes, dst: int) -> None:
-        dist.send(torch.tensor([len(b)], dtype=torch.int64, device=self.local_device), dst)
-        dist.send(_bytes_tensor(b, self.local_device), dst)
+        dist.send(torch.tensor([len(b)], dtype=torch.int64, device=self._wire_device), dst)
+        dist.send(_bytes_tensor(b, self._wire_device), dst)
 
     def _recv_bytes(self, src: int) -> bytes:
-        n = torch.empty(1, dtype=torch.int64, device=self.local_device)
+        n = torch.empty(1, dtype=torch.int64, device=self._wire_device)
         dist.recv(n, src)
-        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=self.local_device)
+        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=self._wire_device)
         dist.recv(buf, src)
         return buf.cpu().numpy().tobytes()
 
@@ -161,7 +190,7 @@ class PipeCommunicator:
                     ctrl += dump_objects(objects, self._meta.object_capacity)
                 else:
                     ctrl += bytes(self._meta.object_capacity)
-                dist.send(_bytes_tensor(ctrl, self.local_device), target_global_rank)
+                dist.send(_bytes_tensor(ctrl, self._wire_device), target_global_rank)
                 changed = not same
             else:
                 if not same or blob != self._object_blob:
@@ -183,7 +212,7 @@ class PipeCommunicator:
         if self._meta is not None:
             if not self.use_continuous_recommunication:
                 return False
-            ctrl = torch.empty(1 + self._meta.object_capacity, dtype=torch.uint8, device=self.local_device)
+            ctrl = torch.empty(1 + self._meta.object_capacity, dtype=torch.uint8, device=self._wire_device)
             dist.recv(ctrl, origin_global_rank)
             cb = ctrl.cpu().numpy().tobytes()
             if cb[0] == 1:
@@ -196,7 +225,19 @@ class PipeCommunicator:
 
     # ------------------------------------------------------------------ p2p
     def _issue(self, ops: list) -> list[Any]:
-        return dist.batch_isend_irecv(ops) if ops else []
+        if not ops:
+            return []
+        if self._host_staged:
+            host_ops, copies = [], []
+            for op in ops:
+                if op.op == dist.isend:
+                    h = op.tensor.to("cpu")
+                else:
+                    h = torch.empty(op.tensor.shape, dtype=op.tensor.dtype)
+                    copies.append((op.tensor, h))
+                host_ops.append(dist.P2POp(op.op, h, op.peer, op.group, op.tag))
+            return [_HostStagedWork(dist.batch_isend_irecv(host_ops), copies)]
+        return dist.batch_isend_irecv(ops)
 
     def wait_pending_sends(self) -> None:
         pending, self._pending = self._pending, []

@@ -84,8 +84,11 @@ class Topology:
 
     # ------------------------------------------------------------------ init
     def initialize_device(self) -> None:
-        if torch.cuda.is_available() and self.config.backend != "gloo":
+        rehearsal = self.config.backend == "gloo" and self.config.gloo_on_gpu
+        if torch.cuda.is_available() and (self.config.backend != "gloo" or rehearsal):
             slot = self.config.local_slot if self.config.local_slot is not None else 0
+            if rehearsal:
+                slot %= torch.cuda.device_count()
             assert slot < torch.cuda.device_count(), (
                 f"cannot assign gpu {slot} for {torch.cuda.device_count()} available gpus"
             )

@@ -89,6 +89,12 @@ class TopologyConfig(BaseConfig):
         description="torch.distributed backend; None selects 'nccl' (RCCL over xGMI) when a GPU is "
         "present and 'gloo' otherwise",
     )
+    gloo_on_gpu: bool = Field(
+        False,
+        description="rehearsal mode: backend 'gloo' with the ranks' tensors on GPUs (local slot modulo the "
+        "visible devices, so several ranks may share one GPU, which RCCL refuses); exercises the GPU-side "
+        "multi-rank paths (streams, events, kernels) on a 1-GPU box",
+    )
 
     @model_validator(mode="before")
     @classmethod

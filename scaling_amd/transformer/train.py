@@ -101,7 +101,19 @@ def main(launch_config: LaunchConfig, overwrite_config: Optional[dict[str, Any]]
         sync_batch_to_model_parallel=_get_sync_batch(context.config.data), loss_function=loss_function,
         metrics_aggregation_fn=metrics_aggregation_fn, dataset_evaluation=val_ds,
     )
-    return trainer.run_training(return_metrics=return_metrics)
+    metrics = trainer.run_training(return_metrics=return_metrics)
+    _shutdown_distributed()
+    return metrics
+
+
+def _shutdown_distributed() -> None:
+    """Every rank leaves together and tears its process group down before interpreter exit: a gloo rank that
+    exits while a peer's transport threads still talk to it can abort that peer (std::terminate)."""
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def _get_sync_batch(data_config: DataConfig) -> Callable:
