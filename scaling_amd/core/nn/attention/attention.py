@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 from enum import Enum
-from typing import Callable, Optional, Union
+from typing import Any, Callable, Optional, Union
 
 import torch
 
@@ -205,6 +205,39 @@ class StaticKVCache:
         return self.k, self.v, self.state.cu_k
 
 
+class _LoraUpInto(torch.autograd.Function):
+    """``base[:, lo:hi] += scaling * h @ B^T`` for each adapter, as GEMMs accumulating straight into the column
+    slices of the q/k/v GEMM output (beta = 1 epilogue: no up-projection tensor, no add pass).  Backward hands
+    the slices of the incoming gradient through without the clone autograd makes for in-place ops on views:
+    dh = scaling * g[:, lo:hi] @ B, dB = scaling * g[:, lo:hi]^T @ h."""
+
+    @staticmethod
+    def forward(ctx: Any, base: torch.Tensor, spec: tuple, *hb: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
+        n = len(spec)
+        hs, bs = hb[:n], hb[n:]
+        b2 = base.view(hs[0].shape[0], -1)
+        for ((lo, hi), sc), h, w in zip(spec, hs, bs):
+            b2[:, lo:hi].addmm_(h, w.t(), alpha=sc)
+        ctx.mark_dirty(base)
+        ctx.spec = spec
+        ctx.save_for_backward(*hs, *bs)
+        return base
+
+    @staticmethod
+    def backward(ctx: Any, g: torch.Tensor):  # type: ignore[override]
+        spec = ctx.spec
+        n = len(spec)
+        saved = ctx.saved_tensors
+        hs, bs = saved[:n], saved[n:]
+        g2 = g.reshape(hs[0].shape[0], -1)
+        dhs, dbs = [], []
+        for i, (((lo, hi), sc), h, w) in enumerate(zip(spec, hs, bs)):
+            gs = g2[:, lo:hi]
+            dhs.append(torch.mm(gs, w) * sc if ctx.needs_input_grad[2 + i] else None)
+            dbs.append(torch.mm(gs.t(), h) * sc if ctx.needs_input_grad[2 + n + i] else None)
+        return (g, None, *dhs, *dbs)
+
+
 class ParallelSelfAttention(torch.nn.Module):
     def __init__(
         self,
@@ -342,21 +375,26 @@ class ParallelSelfAttention(torch.nn.Module):
             qkv = base.view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
             return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :], base
         base = fused_column_linear(x, [self.query, self.key, self.value], self.topology)
+        q, k, v = self._views(base, T)
+        return q, k, v, base
+
+    def _views(self, base: torch.Tensor, T: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
         out = base.view(T, nq * hd + 2 * nkv * hd)
         q = out[:, : nq * hd].view(T, nq, hd)
         k = out[:, nq * hd : (nq + nkv) * hd].view(T, nkv, hd)
         v = out[:, (nq + nkv) * hd :].view(T, nkv, hd)
-        return q, k, v, base
+        return q, k, v
 
     def _fused_rope_attention(self, base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
                               position_ids: Optional[torch.Tensor], s: int, cumulative_seq_lengths: torch.Tensor,
-                              max_seq_length: Optional[int]) -> Optional[torch.Tensor]:
+                              max_seq_length: Optional[int], lora_in_base: bool = False) -> Optional[torch.Tensor]:
         """RoPE + flash attention as one autograd node writing dQKV in place (None if not applicable)."""
         nl = self.num_local_attention_heads
         re = self.rotary_embedding
         if re is None or not self.use_flash_attention or self.key_query_norm:
             return None
-        if self.lora_config is not None and not self.lora_merged_state:
+        if self.lora_config is not None and not self.lora_merged_state and not lora_in_base:
             return None
         pos = position_ids.reshape(-1) if position_ids is not None else None
         return attn_ops.rope_flash_attention(
@@ -365,6 +403,39 @@ class ParallelSelfAttention(torch.nn.Module):
             self.local_attention_window_size if nl > 0 else None,
             dropout_p=self.dropout_attention_probs if self.training else 0.0,
             local_heads=self.num_local_attention_heads_per_partition if nl > 0 else None)
+
+    def _lora_gemm_accumulates(self, m: torch.nn.Module) -> bool:
+        """An adapter whose up-projection can accumulate into the base output (no biases, no active dropout)."""
+        if getattr(m.dense_in, "bias", None) is not None or getattr(m.dense_out, "bias", None) is not None:
+            return False
+        return not (m.dropout is not None and m.dropout.p > 0 and self.training)
+
+    def _lora_into_base(self, x: torch.Tensor, base: torch.Tensor) -> bool:
+        """Unmerged q/k/v adapters at model-parallel size 1 with separate q/k/v weights: ONE down-projection GEMM
+        over the concatenated A matrices (x read once; one input-gradient GEMM and one gradient accumulation into
+        x instead of three), each scaled up-projection added in place into its column slice of the base q/k/v
+        GEMM output — which then takes the fused RoPE + flash path like an adapter-free layer.  Same math as
+        ``apply_lora`` (reference ``attention.py`` LoRA branch); False when not applicable."""
+        cfg = self.lora_config
+        assert cfg is not None
+        mp = self.topology.config.model_parallel_size if self.topology is not None else 1
+        if self.qkv_in_one or mp > 1 or base._base is not None:  # a view output (biased GEMM) cannot be updated in place
+            return False
+        mods = [m for n, m in self.lora_modules.items() if n != f"dense_{cfg.name}"]
+        if not mods:
+            return True
+        if not all(self._lora_gemm_accumulates(m) for m in mods):
+            return False
+        hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
+        cols = {LoRAModuleType.QUERY: (0, nq * hd), LoRAModuleType.KEY: (nq * hd, (nq + nkv) * hd),
+                LoRAModuleType.VALUE: ((nq + nkv) * hd, (nq + 2 * nkv) * hd)}
+        x2 = x.reshape(-1, x.shape[-1])
+        a = torch.cat([m.dense_in.weight for m in mods], dim=0) if len(mods) > 1 else mods[0].dense_in.weight
+        h = torch.nn.functional.linear(x2, a.to(x2.dtype))
+        hs = h.split([m.dense_in.weight.shape[0] for m in mods], dim=1)
+        spec = tuple((cols[m.lora_module_type], m.scaling) for m in mods)
+        _LoraUpInto.apply(base, spec, *hs, *[m.dense_out.weight.to(x2.dtype) for m in mods])
+        return True
 
     def apply_lora(self, x: torch.Tensor, query: torch.Tensor, key: torch.Tensor, value: torch.Tensor) -> list[torch.Tensor]:
         assert self.lora_config is not None
@@ -399,11 +470,16 @@ class ParallelSelfAttention(torch.nn.Module):
         T = b * s
         hd = self.hidden_size_per_attention_head
         q, k, v, base = self._project_base(x)
+        lora_pending = self.lora_config is not None and not self.lora_merged_state
+        lora_in_base = lora_pending and self._lora_into_base(x, base)
+        if lora_in_base:  # fresh views of the updated GEMM output
+            q, k, v = self._views(base, T)
         if not use_cache and not reset_cache and cumulative_seq_lengths_key is None:
-            fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length)
+            fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length,
+                                               lora_in_base=lora_in_base)
             if fused is not None:
                 return self._output(fused.reshape(b, s, -1))
-        if self.lora_config is not None and not self.lora_merged_state:
+        if lora_pending and not lora_in_base:
             q, k, v = self.apply_lora(x, q, k, v)
         if self.key_query_norm:
             assert self.norm_query is not None and self.norm_key is not None
@@ -466,11 +542,19 @@ class ParallelSelfAttention(torch.nn.Module):
 
     def _output(self, hidden: torch.Tensor) -> torch.Tensor:
         dense_lora = None
+        mod = None
         if self.lora_config and not self.lora_merged_state and LoRAModuleType.DENSE in self.lora_config.parallel_modules:
-            dense_lora = self.lora_modules[f"dense_{self.lora_config.name}"](
-                all_concat(hidden, dim=-1, topology=self.topology)
-            )
+            mod = self.lora_modules[f"dense_{self.lora_config.name}"]
+            mp = self.topology.config.model_parallel_size if self.topology is not None else 1
+            if not (mp == 1 and self._lora_gemm_accumulates(mod)):
+                dense_lora = mod(all_concat(hidden, dim=-1, topology=self.topology))
+                mod = None
         out = self.dense(hidden)
+        if mod is not None and out._base is None:  # up-projection GEMM accumulates into the dense output
+            h = torch.nn.functional.linear(hidden.reshape(-1, hidden.shape[-1]), mod.dense_in.weight.to(hidden.dtype))
+            out = _LoraUpInto.apply(out, (((0, out.shape[-1]), mod.scaling),), h, mod.dense_out.weight.to(hidden.dtype))
+        elif mod is not None:
+            dense_lora = mod(hidden)
         if dense_lora is not None:
             out = out + dense_lora
         if self.topology is not None and self.topology.config.sequence_parallel:

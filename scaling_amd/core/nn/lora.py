@@ -60,6 +60,8 @@ class ParallelLoRa(torch.nn.Module):
         x = self.dense_in(x)
         if self.dropout is not None:
             x = self.dropout(x)
+        if getattr(self.dense_out, "bias", None) is None:  # scale the rank-wide intermediate, not the out-wide result (same math)
+            return self.dense_out(x * self.scaling)
         return self.dense_out(x) * self.scaling
 
     def get_delta_weights(self) -> torch.Tensor:

@@ -115,3 +115,76 @@ def test_lora_finetune_dp2_zero(tmp_path: Path):
     ft = _run(tmp_path, cfg, 2, "ft")
     assert len(ft) == 4
     assert _compare(tmp_path, "lora", layer_filter="TransformerLayer") > 0
+
+
+def _in_base_case(modules, kv, device: str, dtype: torch.dtype, kernel: str, rtol: float, atol: float):
+    from scaling_amd.core import LoRaConfig, MaskedSoftmaxConfig, ParallelSelfAttention
+    from scaling_amd.core.nn.attention.attention import RelativePositionEmbeddingType
+    from scaling_amd.core.nn.rotary_config import RotaryConfig
+
+    torch.manual_seed(1234)
+    cfg = LoRaConfig.from_dict({"parallel_modules": modules, "rank": 8, "alpha": 3})
+    attn = ParallelSelfAttention(hidden_size=128, num_attention_heads=4, num_kv_heads=kv, qkv_in_one=False, bias=False,
+                                 lora_config=cfg, masked_softmax_config=MaskedSoftmaxConfig(kernel=kernel),
+                                 relative_position_embedding_type=RelativePositionEmbeddingType.ROTARY,
+                                 rotary_config=RotaryConfig(dimensions=32, max_seq_length=64), dtype=dtype,
+                                 device=torch.device(device))
+    with torch.no_grad():
+        for mod in attn.lora_modules.values():
+            mod.dense_out.weight.copy_(torch.rand_like(mod.dense_out.weight) * 0.1)
+    b, s = 2, 64
+    x0 = torch.randn(b, s, 128, device=device, dtype=dtype)
+    cu = torch.arange(0, (b + 1) * s, s, dtype=torch.int32, device=device)
+    pos = torch.arange(s, device=device).repeat(b, 1)
+    lora_params = [p for n, p in attn.named_parameters() if "lora" in n]
+    wgt = torch.linspace(-1, 1, x0.numel(), device=device, dtype=dtype).view_as(x0)
+
+    def run(in_base: bool):
+        x = x0.clone().requires_grad_(True)
+        calls = []
+        orig = attn._lora_into_base
+
+        def spy(xx, base):
+            r = orig(xx, base) if in_base else False
+            calls.append(r)
+            return r
+
+        attn._lora_into_base = spy
+        if not in_base:  # the unfused reference: no adapter accumulates into a GEMM output (dense included)
+            attn._lora_gemm_accumulates = lambda m: False
+        try:
+            y = attn(x, cumulative_seq_lengths=cu, position_ids=pos)
+        finally:
+            del attn._lora_into_base
+            attn.__dict__.pop("_lora_gemm_accumulates", None)
+        assert calls == [in_base]
+        grads = torch.autograd.grad((y * wgt).sum(), [x, *lora_params])
+        return y.detach().float(), [g.float() for g in grads]
+
+    y_a, g_a = run(True)
+    y_b, g_b = run(False)
+    torch.testing.assert_close(y_a, y_b, rtol=rtol, atol=atol)
+    for ga, gb in zip(g_a, g_b):
+        torch.testing.assert_close(ga, gb, rtol=rtol, atol=atol * max(1.0, gb.abs().max().item()))
+
+
+IN_BASE_MODULES = [["query", "key", "value", "dense"], ["key"], ["query", "value"]]
+
+
+@pytest.mark.parametrize("modules", IN_BASE_MODULES)
+@pytest.mark.parametrize("kv", [None, 2])
+def test_lora_in_base_matches_separate_adds(modules, kv):
+    """The single-GEMM q/k/v adapter path (A matrices concatenated, scaled up-projections accumulated by the GEMM
+    into the base q/k/v output; the dense adapter likewise into the dense output) computes the same outputs and
+    gradients as adapter-by-adapter additions."""
+    _in_base_case(modules, kv, "cpu", torch.float32, "torch", 1e-5, 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("modules", IN_BASE_MODULES)
+@pytest.mark.parametrize("kv", [None, 2])
+def test_lora_in_base_fused_rope_flash_gpu(modules, kv):
+    """On MI355X the in-base adapters feed the fused RoPE + flash-attention node (HIP kernels); the reference
+    is the unfused path (adapter additions, separate RoPE, flash attention) in bf16."""
+    _in_base_case(modules, kv, "cuda", torch.bfloat16, "flash_attention", 2e-2, 2e-2)

@@ -44,6 +44,14 @@ def main() -> None:
     print("| category | ms | % of busy |\n|---|---|---|")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"| {k} | {v:.1f} | {100 * v / busy:.1f} |")
+    if len(sys.argv) > 2:  # top-N kernels of the step by full name
+        per: dict[str, list[float]] = defaultdict(lambda: [0, 0.0])
+        for name, s, e in step:
+            per[name][0] += 1
+            per[name][1] += (e - s) / 1e6
+        print(f"\n| kernel (top {sys.argv[2]}) | calls | ms |\n|---|---|---|")
+        for k, (n, v) in sorted(per.items(), key=lambda kv: -kv[1][1])[: int(sys.argv[2])]:
+            print(f"| {k[:150]} | {n} | {v:.1f} |")
 
 
 if __name__ == "__main__":
