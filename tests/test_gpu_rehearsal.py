@@ -29,6 +29,7 @@ SMALL = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "
         ("4", "1", "2", "1", []),                             # pp2 x dp2, one micro-batch
         ("8", "2", "2", "2", []),                             # tp2 x pp2 x dp2 (BASELINE #3 layout)
         ("4", "1", "1", "2", ["--activation-checkpointing", "every_layer"]),
+        ("2", "1", "1", "2", ["--lora", "--lora-rank", "8"]),         # LoRA fast path under ZeRO dp2
     ],
 )
 def test_bench_rehearsal_gloo_gpu(layout):
