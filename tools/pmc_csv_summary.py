@@ -42,7 +42,9 @@ def main() -> None:
                     continue
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 wall[name][int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    for name, cs in vals.items():
+    order = sorted(vals, key=lambda k: -sum(wall[k].values()))  # heaviest kernels first
+    for name in order:
+        cs = vals[name]
         n = len(wall[name])
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         t = sum(wall[name].values()) / max(1, n)
@@ -63,6 +65,8 @@ def main() -> None:
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_VALU"):
                 if k in avg:
                     d.append(f"{k[3:]}/WAVE {avg[k] / wc:.3f}")
+        if avg.get("FETCH_SIZE") and t > 0:  # FETCH_SIZE is in KiB
+            d.append(f"HBM read {avg['FETCH_SIZE'] * 1024 / t / 1e12:.2f} TB/s")
         if avg.get("SQ_LDS_BANK_CONFLICT") is not None and avg.get("SQ_LDS_IDX_ACTIVE"):
             d.append(f"LDS conflict/active {avg['SQ_LDS_BANK_CONFLICT'] / avg['SQ_LDS_IDX_ACTIVE']:.3f}")
         if d:
