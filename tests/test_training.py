@@ -144,3 +144,23 @@ def test_async_checkpointing_resume_bit_exact(tmp_path):
     cfg["trainer"]["async_checkpointing"] = False
     resumed = _run(tmp_path, cfg, 2, "resumed")
     assert [m["training/loss"] for m in resumed] == [m["training/loss"] for m in full[-4:]]
+
+
+def test_bf16_gradient_reduction_tracks_fp32(tmp_path):
+    """``optimizer.grad_reduce_dtype='bfloat16'`` (bf16 reduce-scatter of the bf16 gradient buckets, then cast and
+    1/dp scale into the fp32 owned shard) trains like the fp32 reduction: same step-1 loss, and later losses within
+    bf16 rounding of the gradients.  Model in bf16 so the bf16 branch is taken."""
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, 1, 1, 2, precision="bfloat16", dropout_embedding=0.0, dropout_attention_probs=0.0,
+                  dropout_after_attention=0.0, dropout_after_mlp=0.0)
+    cfg["trainer"]["save_dir"] = None
+    cfg["trainer"]["load_dir"] = None
+    fp32 = _run(tmp_path, cfg, 2, "fp32")
+    cfg["optimizer"]["grad_reduce_dtype"] = "bfloat16"
+    bf16 = _run(tmp_path, cfg, 2, "bf16")
+    a = np.array([m["training/loss"] for m in fp32])
+    b = np.array([m["training/loss"] for m in bf16])
+    assert np.all(np.isfinite(b))
+    assert a[0] == b[0]
+    assert not np.array_equal(a, b)  # the bf16 reduction path ran (different rounding from step 2 on)
+    assert np.max(np.abs(a - b) / np.abs(a)) < 2e-2, (a, b)
