@@ -67,3 +67,24 @@ def test_rehearsal_tp_loss_matches_single_rank():
     assert all(math.isfinite(v) for v in losses.values()), losses
     for tag in ("tp2", "tp2_sp"):
         assert losses[tag] == pytest.approx(losses["tp1"], rel=2e-2), losses
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("mp,pp,world", [(2, 2, 4), (1, 2, 4), (2, 1, 4)])
+def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
+    """The training entry point (data pipeline -> 3D engine -> ZeRO-1 -> checkpoint at step 6) on GPU ranks sharing
+    the MI355X, bf16 + flash attention: resuming from the step-6 checkpoint reproduces steps 7-10 exactly."""
+    import numpy as np
+
+    from tests.test_training import _config, _make_data, _run as _train
+
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, mp, pp, world, precision="bfloat16", masked_softmax={"kernel": "flash_attention"},
+                  hidden_size=128, sequence_length=128)
+    cfg["topology"]["backend"] = "gloo"
+    cfg["topology"]["gloo_on_gpu"] = True
+    full = _train(tmp_path, cfg, world, "full")
+    assert len(full) == 10 and all(np.isfinite(m["training/loss"]) for m in full)
+    cfg["trainer"]["assert_checkpoint_loaded"] = True
+    resumed = _train(tmp_path, cfg, world, "resumed")
+    assert [m["training/loss"] for m in resumed] == [m["training/loss"] for m in full[-4:]]
