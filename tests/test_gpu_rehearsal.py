@@ -27,7 +27,9 @@ SMALL = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "
         ("2", "2", "1", "2", ["--sequence-parallel"]),        # tp2 + SP, async input-gradient all-reduce
         ("4", "2", "2", "2", []),                             # tp2 x pp2: GPU pipe p2p
         ("4", "1", "2", "1", []),                             # pp2 x dp2, one micro-batch
-        ("8", "2", "2", "2", []),                             # tp2 x pp2 x dp2 (BASELINE #3 layout)
+        ("8", "2", "2", "2", []),                             # tp2 x pp2 x dp2
+        ("8", "2", "2", "2", ["--activation-checkpointing", "every_layer"]),  # BASELINE #4 layout
+        ("8", "2", "1", "1", []),                             # tp2 x dp4 (BASELINE #3 layout)
         ("4", "1", "1", "2", ["--activation-checkpointing", "every_layer"]),
         ("2", "1", "1", "2", ["--lora", "--lora-rank", "8"]),         # LoRA fast path under ZeRO dp2
     ],
