@@ -149,3 +149,22 @@ def test_kv_cache_preallocated_growth():
             assert c.k is buf  # filled in place while capacity lasts
         assert torch.equal(k, torch.cat(ref_k)) and torch.equal(v, torch.cat(ref_v))
     assert c.length == 15 and c.k.shape[0] >= 15
+
+
+def test_llama2_7b_example_config_matches_bench_architecture():
+    """examples/llama2_7b/config.yml trains exactly the architecture bench.py measures."""
+    from pathlib import Path
+
+    from scaling_amd.models import llama_architecture
+    from scaling_amd.transformer import TransformerConfig
+
+    root = Path(__file__).resolve().parent.parent
+    cfg = TransformerConfig.from_yaml(root / "examples" / "llama2_7b" / "config.yml")
+    arch = cfg.transformer_architecture
+    for k, v in llama_architecture("llama2_7b", sequence_length=4096).items():
+        got = getattr(arch, k)
+        got = got.value if hasattr(got, "value") else got
+        if isinstance(v, dict):
+            continue
+        assert got == v, (k, got, v)
+    assert cfg.topology.micro_batch_size * cfg.topology.gradient_accumulation_steps == 8
