@@ -9,6 +9,7 @@ from typing import Any, Optional
 sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 from scaling_amd.core import BaseTrainer, Topology  # noqa: E402
+from scaling_amd.core.topology import shutdown_distributed  # noqa: E402
 from scaling_amd.core.logging import logger  # noqa: E402
 from scaling_amd.core.runner import LaunchConfig  # noqa: E402
 
@@ -38,7 +39,9 @@ def main(launch_config: LaunchConfig, overwrite_config: Optional[dict] = None, r
                           dataset=train_data, dataset_evaluation=valid_data,
                           sync_batch_to_model_parallel=MNISTDataset.sync_batch_to_model_parallel,
                           metrics_aggregation_fn=metrics_aggregation_fn, loss_function=loss_function)
-    return trainer.run_training(return_metrics=return_metrics)
+    metrics = trainer.run_training(return_metrics=return_metrics)
+    shutdown_distributed()
+    return metrics
 
 
 if __name__ == "__main__":

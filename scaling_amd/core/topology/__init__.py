@@ -1,5 +1,5 @@
 from .rng_tracker import CudaRNGStateTracker, RngTrackerState
-from .topology import Topology, TopologyState
+from .topology import Topology, TopologyState, shutdown_distributed
 from .topology_config import ActivationCheckpointingType, PipePartitionMethod, TopologyConfig
 
 __all__ = [
@@ -10,4 +10,5 @@ __all__ = [
     "Topology",
     "TopologyConfig",
     "TopologyState",
+    "shutdown_distributed",
 ]

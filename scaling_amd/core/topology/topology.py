@@ -285,3 +285,11 @@ def env_rank_info() -> dict[str, Any]:
         world_size=int(os.environ.get("WORLD_SIZE", 1)),
         local_slot=int(os.environ.get("LOCAL_SLOT", os.environ.get("LOCAL_RANK", 0))),
     )
+
+
+def shutdown_distributed() -> None:
+    """Every rank leaves together and tears its process group down before interpreter exit: a gloo rank that
+    exits while a peer's transport threads still talk to it can abort that peer (std::terminate)."""
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()

@@ -14,6 +14,7 @@ from typing import Any, Callable, Optional
 import torch
 
 from ..core import BaseBlendedDataset, BaseDataset, DeterminedBaseTrainer, Topology
+from ..core.topology import shutdown_distributed
 from ..core.logging import logger
 from ..core.nn.parallel_module import EvaluationStepOutput, TrainStepOutput
 from ..core.runner.launch_config import LaunchConfig
@@ -102,18 +103,8 @@ def main(launch_config: LaunchConfig, overwrite_config: Optional[dict[str, Any]]
         metrics_aggregation_fn=metrics_aggregation_fn, dataset_evaluation=val_ds,
     )
     metrics = trainer.run_training(return_metrics=return_metrics)
-    _shutdown_distributed()
+    shutdown_distributed()
     return metrics
-
-
-def _shutdown_distributed() -> None:
-    """Every rank leaves together and tears its process group down before interpreter exit: a gloo rank that
-    exits while a peer's transport threads still talk to it can abort that peer (std::terminate)."""
-    import torch.distributed as dist
-
-    if dist.is_initialized():
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 def _get_sync_batch(data_config: DataConfig) -> Callable:
