@@ -344,6 +344,7 @@ def _worker(a: argparse.Namespace) -> None:
                 "world_size_seen": dist.get_world_size(),
                 "per_rank_ms_per_step": [round(1000.0 * float(t) / a.steps, 2) for t in times.tolist()],
                 "dp_param_checksum_agree": dp_agree,
+                "param_checksum": [float(v) for v in ck.tolist()],
                 "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
             },
         }

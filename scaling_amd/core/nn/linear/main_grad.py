@@ -51,6 +51,7 @@ import torch.distributed as dist
 
 from ....ops.gemm import linear as gemm_linear
 from ....ops.gemm import transpose2d, wgrad
+from ...utils.debug_env import side_streams_enabled
 
 _GEN = [0]
 _WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
@@ -63,7 +64,7 @@ _sync_queued = [False]
 
 def wgrad_stream(device: torch.device) -> Optional[Any]:
     """The side stream of this device's GEMM-fused weight-gradient GEMMs (None when disabled / not on a GPU)."""
-    if not _WGRAD_STREAM_ENABLED or device.type != "cuda":
+    if not _WGRAD_STREAM_ENABLED or device.type != "cuda" or not side_streams_enabled():
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _wgrad_streams.get(idx)

@@ -41,6 +41,7 @@ from ..nn.linear.main_grad import invalidate_transposed_weights, sync_wgrad_stre
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
 from ..utils.checkpoint_writer import save_file
+from ..utils.debug_env import side_streams_enabled
 from ..utils.safe_load import safe_load
 from .base import BaseOptimizer, OptimizerStepOutput
 from .loss_scaler import LossScaler
@@ -70,7 +71,8 @@ class Optimizer(BaseOptimizer):
         self.loss_scaler = LossScaler(config=config.loss_scaler, parameter_groups=parameter_groups)
         self.dp = topology.config.data_parallel_size
         self._gpu = topology.device.type == "cuda"
-        self._comm_stream = torch.cuda.Stream(device=topology.device) if (self._gpu and self.dp > 1) else None
+        self._comm_stream = (torch.cuda.Stream(device=topology.device)
+                             if (self._gpu and self.dp > 1 and side_streams_enabled()) else None)
         max_bucket = max(g.bucket_size for g in parameter_groups)
         self._scratch = (
             torch.empty(max_bucket, dtype=torch.float32, device=topology.device)
@@ -260,7 +262,7 @@ class Optimizer(BaseOptimizer):
 
     # ------------------------------------------------------------------ overlapped optimizer step
     def _async_step(self) -> bool:
-        return bool(self._gpu and self.config.overlap_optimizer_step)
+        return bool(self._gpu and self.config.overlap_optimizer_step and side_streams_enabled())
 
     def _step_stream(self) -> Any:
         if self._comm_stream is not None:  # AdamW then the ZeRO all-gather of the bucket, in order, on one stream

@@ -59,7 +59,7 @@ def get_resource_pool(config: RunnerConfig) -> dict[str, list[int]]:
 def _exports(config: Optional[RunnerConfig] = None) -> dict[str, str]:
     env = {k: v for k, v in os.environ.items() if any(k.startswith(p) for p in EXPORT_ENVS)}
     if config is not None:
-        env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking))
+        env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking, config.debug_single_stream))
     extra = Path.home() / ".deepspeed_env"
     if extra.is_file():
         for line in extra.read_text().splitlines():
@@ -108,7 +108,7 @@ def runner_main(config: RunnerConfig, payload: Optional[dict[str, Any]] = None) 
     cmd = PDSHRunner(config, pool, master).get_cmd(payload)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking))
+    env.update(debug_env(config.debug_collectives, config.debug_hip_launch_blocking, config.debug_single_stream))
     proc = subprocess.Popen(cmd, env=env)
     rc = proc.wait()
     if rc != 0:  # the failing rank already printed its error; propagate the code quietly

@@ -32,3 +32,6 @@ class RunnerConfig(BaseConfig, populate_by_name=True):
     debug_hip_launch_blocking: bool = Field(
         False, description="export HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL: synchronous, serialized kernel launches"
     )
+    debug_single_stream: bool = Field(
+        False, description="race check: export SCALING_AMD_SINGLE_STREAM (all side-stream work on the compute stream)"
+    )

@@ -32,12 +32,25 @@ DETERMINISTIC_ENV: Mapping[str, str] = {
 }
 
 
-def debug_env(collectives: bool = False, hip_launch_blocking: bool = False) -> dict[str, str]:
+# race check: every side stream (DP communication, overlapped optimizer step, weight-gradient stream) folds onto
+# the compute stream, so the run is the serialized schedule of the same kernels.  A run whose parameters differ
+# from its SCALING_AMD_SINGLE_STREAM=1 twin has a missing stream / event dependency (tests/test_gpu_rehearsal.py).
+SINGLE_STREAM_ENV: Mapping[str, str] = {"SCALING_AMD_SINGLE_STREAM": "1"}
+
+
+def side_streams_enabled() -> bool:
+    return os.environ.get("SCALING_AMD_SINGLE_STREAM", "0") in ("", "0")
+
+
+def debug_env(collectives: bool = False, hip_launch_blocking: bool = False, single_stream: bool = False
+              ) -> dict[str, str]:
     env: dict[str, str] = {}
     if collectives:
         env.update(COLLECTIVE_DEBUG_ENV)
     if hip_launch_blocking:
         env.update(HIP_LAUNCH_DEBUG_ENV)
+    if single_stream:
+        env.update(SINGLE_STREAM_ENV)
     return env
 
 

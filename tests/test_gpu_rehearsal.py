@@ -90,3 +90,29 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
     cfg["trainer"]["assert_checkpoint_loaded"] = True
     resumed = _train(tmp_path, cfg, world, "resumed")
     assert [m["training/loss"] for m in resumed] == [m["training/loss"] for m in full[-4:]]
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize(
+    "args,env",
+    [
+        (["--gpus", "1", "--backend", "auto"], {}),                            # overlapped step on its side stream
+        (["--gpus", "1", "--backend", "auto"], {"SCALING_AMD_WGRAD_STREAM": "1"}),  # + weight-gradient stream
+        (["--gpus", "2"], {}),                                                 # DP comm stream
+        (["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {}),
+    ],
+)
+def test_race_check_multi_stream_equals_single_stream(args, env):
+    """Race check: the multi-stream schedule (DP communication stream, overlapped optimizer step,
+    optional weight-gradient stream, per-layer event waits) must leave bit-identical parameters and losses to
+    the same run with every side stream folded onto the compute stream (SCALING_AMD_SINGLE_STREAM=1).  A missing
+    stream / event dependency shows up as a different checksum."""
+    base = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
+            "--warmup", "1"]
+    out = {}
+    for mode, extra in (("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})):
+        r = _run([*base, *args], env_extra={**env, **extra}, timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+        res = _json_lines(r.stdout)[0]["config"]
+        out[mode] = (res["param_checksum"], res["loss"])
+    assert out["multi"] == out["single"], out

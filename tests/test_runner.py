@@ -79,3 +79,13 @@ def test_runner_debug_and_determinism_env(monkeypatch):
     import os
 
     assert os.environ["ROCBLAS_DEFAULT_ATOMICS_MODE"] == "0" and os.environ["PYTORCH_TUNABLEOP_TUNING"] == "0"
+
+
+def test_single_stream_race_check_switch(monkeypatch):
+    from scaling_amd.core.utils.debug_env import debug_env, side_streams_enabled
+
+    monkeypatch.delenv("SCALING_AMD_SINGLE_STREAM", raising=False)
+    assert side_streams_enabled()
+    monkeypatch.setenv("SCALING_AMD_SINGLE_STREAM", "1")
+    assert not side_streams_enabled()
+    assert debug_env(single_stream=True) == {"SCALING_AMD_SINGLE_STREAM": "1"}
