@@ -116,3 +116,31 @@ def test_race_check_multi_stream_equals_single_stream(args, env):
         res = _json_lines(r.stdout)[0]["config"]
         out[mode] = (res["param_checksum"], res["loss"])
     assert out["multi"] == out["single"], out
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("before,after", [((2, 2, 8), (1, 1, 1)), ((1, 1, 1), (2, 2, 8)), ((1, 2, 4), (2, 1, 4))])
+def test_rehearsal_layout_change_resume_gpu(tmp_path, before, after):
+    """Layout-independent checkpoints on GPU ranks (bf16, flash attention, ZeRO-1): saved at step 6 under one
+    (TP, PP, world) layout, resumed under another, the run continues (reference tolerance: 15 % on the loss;
+    global batch kept constant through the data-parallel size x gradient accumulation)."""
+    from tests.test_training import _config, _make_data, _run as _train
+
+    _make_data(tmp_path / "data")
+
+    def cfg_for(mp, pp, world):
+        c = _config(tmp_path, mp, pp, world, precision="bfloat16", masked_softmax={"kernel": "flash_attention"},
+                    hidden_size=128, sequence_length=128)
+        dp = world // (mp * pp)
+        c["topology"]["gradient_accumulation_steps"] = 4 // dp if dp <= 4 else 1
+        c["topology"]["backend"] = "gloo"
+        c["topology"]["gloo_on_gpu"] = True
+        return c
+
+    full = _train(tmp_path, cfg_for(*before), before[2], "full")
+    c2 = cfg_for(*after)
+    c2["trainer"]["assert_checkpoint_loaded"] = True
+    resumed = _train(tmp_path, c2, after[2], "resumed")
+    a = [m["training/loss"] for m in full][-4:]
+    b = [m["training/loss"] for m in resumed]
+    assert len(b) == 4 and all(abs(x - y) / x < 0.15 for x, y in zip(a, b)), (a, b)
