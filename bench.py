@@ -364,6 +364,10 @@ def _worker(a: argparse.Namespace) -> None:
 
 def main() -> None:
     a = _args()
+    if a.lora and a.gemm_tuning == "tune":
+        # the LoRA path's GEMMs write / read column slices (ld > n): TunableOp's tuning pass mis-handles them
+        # (invalid-argument errors and non-finite results measured on MI355X); tune on the full-training path
+        raise SystemExit("bench.py: --gemm-tuning tune is not supported with --lora")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(_launch(a))
     _worker(a)
