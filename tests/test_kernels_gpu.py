@@ -689,3 +689,34 @@ def test_gemv_rejects_unsupported():
     assert not ext().gemv_ok(x, w)  # more than 4 rows: hipBLASLt
     assert not ext().gemv_ok(x[:1, :60], w[:, :60])  # K % 8
     assert not ext().gemv_ok(x[:1].float(), w.float())  # fp32
+
+
+@pytest.mark.parametrize("layer", [False, True])
+@pytest.mark.parametrize("rows", [1, 2, 3, 4])
+@pytest.mark.parametrize("H", [4096, 2048, 8192, 520])
+def test_norm_decode_rows_kernel(layer, rows, H):
+    """Decode-sized rows (<= 4) run the one-workgroup-per-row forward kernel: same outputs as the fp32 reference
+    (plain and residual-fused), the residual sum bit-exact, and rstd / mean saved for the backward."""
+    torch.manual_seed(3)
+    dtype = torch.bfloat16
+    x = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
+    r = torch.randn(rows, H, device=DEV, dtype=dtype)
+    w = (1 + 0.1 * torch.randn(H, device=DEV, dtype=dtype))
+    b = 0.1 * torch.randn(H, device=DEV, dtype=dtype)
+    tol = 2e-2
+    y = norm.layer_norm(x, w, b, 1e-5) if layer else norm.rms_norm(x, w, 1e-5)
+    xr, wr, br = x.detach().float(), w.float(), b.float()
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5) if layer else norm.rms_norm_reference(xr, wr, 1e-5)
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    s, y2 = norm.add_layer_norm(x, r, w, b, 1e-5) if layer else norm.add_rms_norm(x, r, w, 1e-5)
+    sr = (x.detach() + r).float()
+    torch.testing.assert_close(s.float(), sr, atol=0, rtol=0)
+    yr2 = torch.nn.functional.layer_norm(sr, (H,), wr, br, 1e-5) if layer else norm.rms_norm_reference(sr, wr, 1e-5)
+    torch.testing.assert_close(y2.float(), yr2, atol=tol, rtol=tol)
+    g = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, x, g)  # the backward reads the rstd / mean the row kernel stored
+    xr2 = x.detach().float().requires_grad_(True)
+    yr3 = (torch.nn.functional.layer_norm(xr2, (H,), wr, br, 1e-5) if layer
+           else norm.rms_norm_reference(xr2, wr, 1e-5))
+    (gr,) = torch.autograd.grad(yr3, xr2, g.float())
+    torch.testing.assert_close(gx.float(), gr, atol=4e-2, rtol=4e-2)
