@@ -87,25 +87,23 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
     }
 }
 
-// Decode-sized forward (rows <= 4, one token per sequence): the whole 4-wave workgroup on ONE row, so a row's loads
-// are issued by 256 lanes at once, and the weight (and bias) are fetched together with x before the reduction —
-// one memory round trip instead of the one-wave kernel's two; cross-wave sum through LDS.  Same math and rounding
-// as norm_fwd_kernel.
+// Decode-sized forward (rows <= 4, one token per sequence): one wave per row as in norm_fwd_kernel (same lane ->
+// element assignment and summation order, so results are bit-identical to it), but the weight (and bias) loads are
+// issued together with x before the reduction: one memory round trip instead of two on a latency-bound launch.
 template <typename T, int NV, bool LAYER>
-__global__ __launch_bounds__(256) void norm_fwd_row_kernel(const T* __restrict__ x, const T* __restrict__ w,
-                                                           const T* __restrict__ b, T* __restrict__ y,
-                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                           int H, float eps, const T* __restrict__ res,
-                                                           T* __restrict__ sum_out) {
-    __shared__ float red[2][4];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+__global__ __launch_bounds__(64) void norm_fwd_row_kernel(const T* __restrict__ x, const T* __restrict__ w,
+                                                          const T* __restrict__ b, T* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          int H, float eps, const T* __restrict__ res,
+                                                          T* __restrict__ sum_out) {
+    const int lane = threadIdx.x;
     const int64_t row = blockIdx.x;
     const T* xr = x + row * H;
     float v[NV][8], wr[NV][8], br[NV][8];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        const int c = (i * 256 + tid) * 8;
+        const int c = (i * 64 + lane) * 8;
         if (c < H) {
             V8<T>::ld(xr + c, v[i]);
             V8<T>::ld(w + c, wr[i]);
@@ -125,25 +123,19 @@ __global__ __launch_bounds__(256) void norm_fwd_row_kernel(const T* __restrict__
         }
     }
     s = wave_sum(s);
-    if (lane == 0) red[0][wv] = s;
-    __syncthreads();
-    s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     float mean = 0.f, rstd;
     if (LAYER) {
         mean = s / H;
         float q = 0.f;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-            const int c = (i * 256 + tid) * 8;
+            const int c = (i * 64 + lane) * 8;
             if (c < H) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; q += d * d; }
             }
         }
         q = wave_sum(q);
-        if (lane == 0) red[1][wv] = q;
-        __syncthreads();
-        q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
         rstd = rsqrtf(q / H + eps);
     } else {
         rstd = rsqrtf(s / H + eps);
@@ -151,7 +143,7 @@ __global__ __launch_bounds__(256) void norm_fwd_row_kernel(const T* __restrict__
     T* yr = y + row * H;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-        const int c = (i * 256 + tid) * 8;
+        const int c = (i * 64 + lane) * 8;
         if (c < H) {
             float o[8];
             if (LAYER) {
@@ -164,7 +156,7 @@ __global__ __launch_bounds__(256) void norm_fwd_row_kernel(const T* __restrict__
             V8<T>::st(yr + c, o);
         }
     }
-    if (tid == 0) {
+    if (lane == 0) {
         rstd_out[row] = rstd;
         if (LAYER) mean_out[row] = mean;
     }
@@ -345,11 +337,12 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
     IO<T>::st(out, c, s);
 }
 
-// SCALING_AMD_NORM_ROW_KERNEL=0 keeps decode-sized rows on the one-wave-per-row kernel (A/B switch)
+// SCALING_AMD_NORM_ROW_KERNEL=1 routes decode-sized rows to the early-weight-load row kernel (opt-in until its
+// bit-identity test has run on the GPU; SCALING_AMD_NORM_ROW_KERNEL=0 / unset keeps the many-row kernel)
 static bool row_kernel_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("SCALING_AMD_NORM_ROW_KERNEL");
-        return !(e != nullptr && e[0] == '0');
+        return e != nullptr && e[0] == '1';
     }();
     return on;
 }
@@ -359,14 +352,14 @@ static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, f
                          int H, float eps, const void* res, void* sum_out, hipStream_t st) {
     const int nv = (H + 511) / 512;
     dim3 grid(cdiv(rows, 4)), block(256);
-    if (rows <= 4 && H <= 8192 && row_kernel_enabled()) {  // decode-sized
-        const int nr = (H + 2047) / 2048;
+    if (rows <= 4 && H <= 4096 && row_kernel_enabled()) {  // decode-sized (NV <= 8)
 #define SA_NR(N)                                                                                                   \
-    hipLaunchKernelGGL((norm_fwd_row_kernel<T, N, LAYER>), dim3((unsigned)rows), block, 0, st, (const T*)x,         \
+    hipLaunchKernelGGL((norm_fwd_row_kernel<T, N, LAYER>), dim3((unsigned)rows), dim3(64), 0, st, (const T*)x,      \
                        (const T*)w, (const T*)b, (T*)y, mean, rstd, H, eps, (const T*)res, (T*)sum_out)
-        if (nr <= 1) SA_NR(1);
-        else if (nr <= 2) SA_NR(2);
-        else SA_NR(4);
+        if (nv <= 1) SA_NR(1);
+        else if (nv <= 2) SA_NR(2);
+        else if (nv <= 4) SA_NR(4);
+        else SA_NR(8);
 #undef SA_NR
         return;
     }

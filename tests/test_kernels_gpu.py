@@ -695,8 +695,8 @@ def test_gemv_rejects_unsupported():
 @pytest.mark.parametrize("rows", [1, 2, 3, 4])
 @pytest.mark.parametrize("H", [4096, 2048, 8192, 520])
 def test_norm_decode_rows_kernel(layer, rows, H):
-    """Decode-sized rows (<= 4) run the one-workgroup-per-row forward kernel: same outputs as the fp32 reference
-    (plain and residual-fused), the residual sum bit-exact, and rstd / mean saved for the backward."""
+    """Decode-sized rows (<= 4) run the early-weight-load row kernel: same outputs as the fp32 reference (plain and
+    residual-fused), bit-identical to the many-row kernel, and rstd / mean saved for the backward."""
     torch.manual_seed(3)
     dtype = torch.bfloat16
     x = torch.randn(rows, H, device=DEV, dtype=dtype, requires_grad=True)
@@ -713,6 +713,13 @@ def test_norm_decode_rows_kernel(layer, rows, H):
     torch.testing.assert_close(s.float(), sr, atol=0, rtol=0)
     yr2 = torch.nn.functional.layer_norm(sr, (H,), wr, br, 1e-5) if layer else norm.rms_norm_reference(sr, wr, 1e-5)
     torch.testing.assert_close(y2.float(), yr2, atol=tol, rtol=tol)
+    # bit-identical to the many-row kernel (same per-lane summation order): rows of a 5-row call
+    x5 = torch.cat([x.detach(), torch.randn(1, H, device=DEV, dtype=dtype)])
+    r5 = torch.cat([r, torch.randn(1, H, device=DEV, dtype=dtype)])
+    y5 = norm.layer_norm(x5, w, b, 1e-5) if layer else norm.rms_norm(x5, w, 1e-5)
+    assert torch.equal(y5[:rows], y.detach())
+    s5, y25 = norm.add_layer_norm(x5, r5, w, b, 1e-5) if layer else norm.add_rms_norm(x5, r5, w, 1e-5)
+    assert torch.equal(y25[:rows], y2.detach()) and torch.equal(s5[:rows], s.detach())
     g = torch.randn_like(y)
     (gx,) = torch.autograd.grad(y, x, g)  # the backward reads the rstd / mean the row kernel stored
     xr2 = x.detach().float().requires_grad_(True)
