@@ -337,12 +337,11 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
     IO<T>::st(out, c, s);
 }
 
-// SCALING_AMD_NORM_ROW_KERNEL=1 routes decode-sized rows to the early-weight-load row kernel (opt-in until its
-// bit-identity test has run on the GPU; SCALING_AMD_NORM_ROW_KERNEL=0 / unset keeps the many-row kernel)
+// SCALING_AMD_NORM_ROW_KERNEL=0 keeps decode-sized rows on the many-row kernel (A/B switch; results are bit-identical)
 static bool row_kernel_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("SCALING_AMD_NORM_ROW_KERNEL");
-        return e != nullptr && e[0] == '1';
+        return !(e != nullptr && e[0] == '0');
     }();
     return on;
 }
