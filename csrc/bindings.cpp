@@ -278,7 +278,7 @@ void ar_close(int64_t ptr) { (void)hipIpcCloseMemHandle(reinterpret_cast<void*>(
 void ar_free(int64_t ptr) { (void)hipFree(reinterpret_cast<void*>((uintptr_t)ptr)); }
 // x (+)= sum over ranks, in place; x is first copied into this rank's slot `slot_off`
 void ar_allreduce(at::Tensor x, const std::vector<int64_t>& bases, int64_t rank, int64_t slot_off, int64_t flag_off,
-                  int64_t epoch, bool signal, at::Tensor err) {
+                  int64_t epoch, bool signal, at::Tensor err, int64_t max_spins) {
     check_cuda(x, "x");
     TORCH_CHECK(x.is_contiguous(), "ar_allreduce: contiguous input");
     TORCH_CHECK(bases.size() >= 1 && bases.size() <= 8 && rank >= 0 && rank < (int64_t)bases.size(), "ar_allreduce: ranks");
@@ -292,7 +292,7 @@ void ar_allreduce(at::Tensor x, const std::vector<int64_t>& bases, int64_t rank,
     std::vector<char*> b(bases.size());
     for (size_t i = 0; i < bases.size(); ++i) b[i] = reinterpret_cast<char*>((uintptr_t)bases[i]);
     sa_launch::oneshot_allreduce(dt(x), b.data(), (int)bases.size(), (int)rank, slot_off, flag_off, (uint32_t)epoch,
-                                 signal, x.data_ptr(), x.numel(), err.data_ptr<int>(), cur_stream());
+                                 signal, x.data_ptr(), x.numel(), err.data_ptr<int>(), max_spins, cur_stream());
 }
 
 // ------------------------------------------------------------------ transpose (dgrad weight cache)
@@ -548,6 +548,8 @@ at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind) {
     return dx;
 }
 // out = res + dropout(x); res optional (plain dropout).  Backward = dropout(g) with the same seed.
+void spin_us(int64_t us) { sa_launch::spin(us, cur_stream()); }
+
 at::Tensor dropout_add(const at::Tensor& x_, const c10::optional<at::Tensor>& res_, double p, int64_t seed) {
     TORCH_CHECK(x_.is_cuda(), "dropout: GPU tensor expected");
     TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout: probability must be in [0, 1)");
@@ -578,7 +580,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("ar_open", &ar_open, "one-shot all-reduce: map a peer's registered buffer");
     m.def("ar_close", &ar_close, "unmap a peer buffer");
     m.def("ar_free", &ar_free, "free an own registered buffer");
-    m.def("ar_allreduce", &ar_allreduce, "one-shot all-reduce of x over the registered buffers (in place)");
+    m.def("ar_allreduce", &ar_allreduce, "one-shot all-reduce of x over the registered buffers (in place)",
+          py::arg("x"), py::arg("bases"), py::arg("rank"), py::arg("slot_off"), py::arg("flag_off"), py::arg("epoch"),
+          py::arg("signal"), py::arg("err"), py::arg("max_spins") = int64_t(1) << 26);
     m.def("transpose_ok", &transpose_ok, "whether transpose2d supports this tensor");
     m.def("transpose2d", &transpose2d, "x^T (contiguous) for 2-byte 2-D matrices");
     m.def("gemv_ok", &gemv_ok, "whether gemv supports these operands");
@@ -597,6 +601,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("masked_softmax_bwd", &masked_softmax_bwd, "masked softmax backward", py::arg("dy"), py::arg("y"), py::arg("mask"), py::arg("scale"));
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
+    m.def("spin_us", &spin_us, "debug: busy-wait kernel of ~us microseconds on the current stream");
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
     m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("max_k") = -1);
     m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);

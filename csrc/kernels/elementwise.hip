@@ -228,6 +228,13 @@ __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, c
         }
 }
 
+// debug: one wave that busy-waits `ticks` of the constant 100 MHz wall clock (s_memrealtime), so a stream carrying
+// it runs ~late; used to delay the DP communication stream in race checks (SCALING_AMD_COMM_DELAY_US)
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
 int ew_grid(int64_t n) {
     const int64_t blocks = (n / 8 + 255) / 256;
     return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 256 * 16));
@@ -296,6 +303,9 @@ void act_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t n, int 
     else if (dtype == DT_F16)
         hipLaunchKernelGGL(act_bwd_kernel<_Float16>, g, 256, 0, st, (const _Float16*)dy, (const _Float16*)x, (_Float16*)dx, n, kind);
     else hipLaunchKernelGGL(act_bwd_kernel<float>, g, 256, 0, st, (const float*)dy, (const float*)x, (float*)dx, n, kind);
+}
+void spin(int64_t us, hipStream_t st) {
+    if (us > 0) hipLaunchKernelGGL(spin_kernel, 1, 64, 0, st, (uint64_t)us * 100);
 }
 void dropout(int dtype, const void* x, const void* res, void* out, int64_t n, uint32_t seed, uint32_t thr, float rp,
              hipStream_t st) {

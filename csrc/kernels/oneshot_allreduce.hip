@@ -7,8 +7,11 @@
 //   2. block 0 publishes it: system-scope release, then epoch -> flag[my rank] in every PEER's flag row
 //      (vector stores over xGMI);
 //   3. every block waits until its own flag row holds `epoch` from all ranks (bounded spin: on timeout it
-//      records an error word and leaves, so a missing peer cannot hang the GPU), system-scope acquire;
+//      records an error word, skips the sum and fills its part of the output with NaN, so a missing peer can
+//      neither hang the GPU nor turn stale slots into plausible numbers), system-scope acquire;
 //   4. each thread sums its 16-B chunks from all ranks' slots in fp32 and writes the result.
+// The error word is read back at the optimizer's per-step host sync (custom_allreduce.pending_error_words),
+// which raises: a timeout is never silent.
 // Double-buffered slots make one barrier per call sufficient: a peer that reached call e's barrier has
 // finished reading call e-1, whose slot call e+1 reuses.  All flag traffic uses vector memory instructions.
 #include <algorithm>
@@ -71,7 +74,10 @@ struct Peers {
 template <typename T>
 __global__ __launch_bounds__(256) void oneshot_allreduce_kernel(Peers peers, int world, int rank, int64_t slot_off,
                                                                 int64_t flag_off, uint32_t epoch, int signal,
-                                                                void* __restrict__ out, int64_t n, int* err) {
+                                                                void* __restrict__ out, int64_t n, int* err,
+                                                                int64_t max_spins) {
+    __shared__ int timed_out;
+    if (threadIdx.x == 0) timed_out = 0;
     if (signal) {
         if (blockIdx.x == 0 && threadIdx.x < world) {
             __atomic_thread_fence(__ATOMIC_RELEASE);  // the slot copy happened earlier on this stream
@@ -85,18 +91,28 @@ __global__ __launch_bounds__(256) void oneshot_allreduce_kernel(Peers peers, int
                 int64_t spins = 0;
                 while (__hip_atomic_load(mine + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
                     __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (int64_t(1) << 26)) {  // ~seconds: a peer never arrived
+                    if (++spins > max_spins) {  // (default ~seconds) a peer never arrived
                         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        timed_out = 1;
                         break;
                     }
                 }
+                if (timed_out) break;
             }
             __threadfence_system();
         }
-        __syncthreads();
     }
+    __syncthreads();
     constexpr int V = Vec<T>::N;
     const int64_t nvec = n / V;
+    if (timed_out) {  // the peers' slots may hold an earlier call's data: poison instead of summing it
+        float nan[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) nan[j] = __builtin_nanf("");
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x)
+            Vec<T>::st(reinterpret_cast<char*>(out) + i * V * (int64_t)sizeof(T), nan);
+        return;
+    }
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
         float acc[V];
 #pragma unroll
@@ -113,7 +129,8 @@ __global__ __launch_bounds__(256) void oneshot_allreduce_kernel(Peers peers, int
 
 namespace sa_launch {
 void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64_t slot_off, int64_t flag_off,
-                       uint32_t epoch, bool signal, void* out, int64_t n, int* err, hipStream_t st) {
+                       uint32_t epoch, bool signal, void* out, int64_t n, int* err, int64_t max_spins,
+                       hipStream_t st) {
     Peers p{};
     for (int i = 0; i < world && i < kMaxRanks; ++i) p.base[i] = bases[i];
     const int vec = dtype == DT_F32 ? 4 : 8;
@@ -121,12 +138,12 @@ void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64
     const int grid = (int)std::min<int64_t>(std::max<int64_t>((nvec + 255) / 256, 1), 1024);
     if (dtype == DT_BF16)
         hipLaunchKernelGGL(oneshot_allreduce_kernel<u16>, grid, 256, 0, st, p, world, rank, slot_off, flag_off, epoch,
-                           signal ? 1 : 0, out, n, err);
+                           signal ? 1 : 0, out, n, err, max_spins);
     else if (dtype == DT_F16)
         hipLaunchKernelGGL(oneshot_allreduce_kernel<_Float16>, grid, 256, 0, st, p, world, rank, slot_off, flag_off, epoch,
-                           signal ? 1 : 0, out, n, err);
+                           signal ? 1 : 0, out, n, err, max_spins);
     else
         hipLaunchKernelGGL(oneshot_allreduce_kernel<float>, grid, 256, 0, st, p, world, rank, slot_off, flag_off, epoch,
-                           signal ? 1 : 0, out, n, err);
+                           signal ? 1 : 0, out, n, err, max_spins);
 }
 }  // namespace sa_launch

@@ -54,10 +54,12 @@ def get_max_seq_length(cumulative_seq_lengths: torch.Tensor) -> int:
 
 
 def _segment_ids(cu: torch.Tensor, total: int) -> torch.Tensor:
-    ids = torch.zeros(total, dtype=torch.long, device=cu.device)
-    if cu.numel() > 2:
-        ids.index_add_(0, cu[1:-1].long(), torch.ones(cu.numel() - 2, dtype=torch.long, device=cu.device))
-    return ids.cumsum(0)
+    """Segment index of every token (number of interior boundaries <= position): a sorted search, which is
+    deterministic under ``torch.use_deterministic_algorithms`` (a scatter-add such as ``index_add_`` is not on GPU)."""
+    pos = torch.arange(total, dtype=torch.long, device=cu.device)
+    if cu.numel() <= 2:
+        return torch.zeros_like(pos)
+    return torch.searchsorted(cu[1:-1].long().contiguous(), pos, right=True)
 
 
 def cumulative_seq_lengths_to_dense_attention_mask(

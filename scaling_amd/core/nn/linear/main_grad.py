@@ -59,7 +59,7 @@ _WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
 
 _WGRAD_STREAM_ENABLED = os.environ.get("SCALING_AMD_WGRAD_STREAM", "0") == "1"
 _wgrad_streams: dict[int, Any] = {}
-_sync_queued = [False]
+_sync_queued = [-1]  # autograd graph task id whose end-of-backward sync is queued
 
 
 def wgrad_stream(device: torch.device) -> Optional[Any]:
@@ -84,12 +84,15 @@ def sync_wgrad_stream(device: torch.device) -> None:
 
 
 def _queue_end_of_backward_sync(device: torch.device) -> None:
-    if _sync_queued[0]:
+    # keyed by the autograd graph task: a backward that raised before its final callbacks ran leaves a stale id,
+    # which the next backward (a new task id) simply does not match, so its sync is still queued
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and _sync_queued[0] == task:
         return
-    _sync_queued[0] = True
+    _sync_queued[0] = task
 
     def _sync() -> None:
-        _sync_queued[0] = False
+        _sync_queued[0] = -1
         sync_wgrad_stream(device)
 
     torch.autograd.Variable._execution_engine.queue_callback(_sync)

@@ -20,7 +20,9 @@ MI355X-first protocol (the reference sends a blocking message per tensor):
   activation receives take fresh blocks from the caching allocator because the pipeline keeps
   several in flight for their backward;
 * python objects are exchanged with the meta; in fixed-meta mode they must stay equal (like the
-  reference's shape assert), in continuous mode they ride in the per-message control blob.
+  reference's shape assert), in continuous mode they ride in the per-message control blob;
+* metadata and control blobs use the same batched, non-blocking sends as the payloads (no blocking
+  ``dist.send`` while batched sends are in flight): one ordered p2p stream per peer.
 """
 from __future__ import annotations
 
@@ -160,15 +162,24 @@ class PipeCommunicator:
         """Device of the (rare) metadata messages: host memory when gloo carries them."""
         return torch.device("cpu") if self._host_staged else self.local_device
 
+    # Every message of the protocol -- metadata, continuous-recommunication control blobs and payloads -- goes
+    # through batch_isend_irecv: there is no blocking dist.send/recv interleaved with in-flight batched sends, so
+    # on RCCL all traffic to a peer is one ordered stream of grouped p2p calls on the communicator.
+    def _send_wire(self, tensors: list[torch.Tensor], dst: int) -> None:
+        self._park(self._issue([dist.P2POp(dist.isend, t, dst) for t in tensors]), tensors)
+
+    def _recv_wire(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        for w in self._issue([dist.P2POp(dist.irecv, t, src)]):
+            w.wait()
+        return t
+
     def _send_bytes(self, b: bytes, dst: int) -> None:
-        dist.send(torch.tensor([len(b)], dtype=torch.int64, device=self._wire_device), dst)
-        dist.send(_bytes_tensor(b, self._wire_device), dst)
+        hdr = torch.tensor([len(b)], dtype=torch.int64, device=self._wire_device)
+        self._send_wire([hdr, _bytes_tensor(b, self._wire_device)], dst)
 
     def _recv_bytes(self, src: int) -> bytes:
-        n = torch.empty(1, dtype=torch.int64, device=self._wire_device)
-        dist.recv(n, src)
-        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=self._wire_device)
-        dist.recv(buf, src)
+        n = self._recv_wire(torch.empty(1, dtype=torch.int64, device=self._wire_device), src)
+        buf = self._recv_wire(torch.empty(int(n.item()), dtype=torch.uint8, device=self._wire_device), src)
         return buf.cpu().numpy().tobytes()
 
     def send_meta(self, data: Any, target_global_rank: int) -> tuple[list[torch.Tensor], bool]:
@@ -190,7 +201,7 @@ class PipeCommunicator:
                     ctrl += dump_objects(objects, self._meta.object_capacity)
                 else:
                     ctrl += bytes(self._meta.object_capacity)
-                dist.send(_bytes_tensor(ctrl, self._wire_device), target_global_rank)
+                self._send_wire([_bytes_tensor(ctrl, self._wire_device)], target_global_rank)
                 changed = not same
             else:
                 if not same or blob != self._object_blob:
@@ -212,8 +223,8 @@ class PipeCommunicator:
         if self._meta is not None:
             if not self.use_continuous_recommunication:
                 return False
-            ctrl = torch.empty(1 + self._meta.object_capacity, dtype=torch.uint8, device=self._wire_device)
-            dist.recv(ctrl, origin_global_rank)
+            ctrl = self._recv_wire(torch.empty(1 + self._meta.object_capacity, dtype=torch.uint8,
+                                               device=self._wire_device), origin_global_rank)
             cb = ctrl.cpu().numpy().tobytes()
             if cb[0] == 1:
                 if self._meta.object_capacity:

@@ -36,12 +36,13 @@ import torch
 import torch.distributed as dist
 
 from ...ops import optim as optim_ops
+from ...parallel import custom_allreduce
 from ..logging import logger
 from ..nn.linear.main_grad import invalidate_transposed_weights, sync_wgrad_stream, wgrad_stream
 from ..nn.parameter_meta import CoreParameterMeta
 from ..utils.param_merge import merge_parameter, split_parameter
 from ..utils.checkpoint_writer import save_file
-from ..utils.debug_env import side_streams_enabled
+from ..utils.debug_env import comm_delay_us, side_streams_enabled
 from ..utils.safe_load import safe_load
 from .base import BaseOptimizer, OptimizerStepOutput
 from .loss_scaler import LossScaler
@@ -175,6 +176,7 @@ class Optimizer(BaseOptimizer):
         inv = 1.0 / self.dp
 
         def run() -> None:
+            self._debug_delay()
             src = g.bucket_view(g.flat_grad, b)
             out = g.owned_view(g.owned_grad, b)
             if self.config.zero:
@@ -200,6 +202,15 @@ class Optimizer(BaseOptimizer):
         else:
             sync_wgrad_stream(self.topology.device)
             run()
+
+    def _debug_delay(self) -> None:
+        """Race-check switch (``SCALING_AMD_COMM_DELAY_US``): a busy-wait kernel on the current (communication)
+        stream in front of a collective."""
+        us = comm_delay_us()
+        if us and self._gpu:
+            from ...ops._ext import ext
+
+            ext().spin_us(us)
 
     def prepare_grad_sync(self) -> None:
         """Called by the engine right before the last micro-batch backward of this stage."""
@@ -252,12 +263,20 @@ class Optimizer(BaseOptimizer):
             if mp_rank != 0:
                 for s, _, n in g.dup_owned_ranges:
                     optim_ops.sumsq_nonfinite_(src[s : s + n], acc[2:4], inv_scale, accumulate=True)
-        vals = torch.stack([acc[0] - acc[2], acc[1]]).double()
+        # third slot: error words of the one-shot TP all-reduce (a peer timeout poisons its output with NaN and
+        # sets the word); always present so every rank all-reduces the same shape
+        errs = custom_allreduce.pending_error_words()
+        err = torch.stack(errs).sum().float() if errs else torch.zeros((), dtype=torch.float32, device=dev)
+        vals = torch.stack([acc[0] - acc[2], acc[1], err.to(acc.device)]).double()
         if not self.config.zero and self.dp > 1:
-            vals = vals / self.dp  # every dp rank holds the full (identical) reduced gradient
+            vals[:2] = vals[:2] / self.dp  # every dp rank holds the full (identical) reduced gradient
         if dist.is_initialized() and dist.get_world_size() > 1:
             dist.all_reduce(vals)
         v = vals.tolist()
+        if v[2] > 0:
+            custom_allreduce.reset_error_words()
+            raise RuntimeError("one-shot tensor-parallel all-reduce timed out waiting for a peer on some rank; "
+                               "its outputs were poisoned (NaN) and this step's gradients are invalid")
         return float(v[0]), float(v[1])
 
     # ------------------------------------------------------------------ overlapped optimizer step
@@ -317,6 +336,7 @@ class Optimizer(BaseOptimizer):
             assert self._comm_stream is not None
             self._comm_stream.wait_stream(torch.cuda.current_stream(self.topology.device))
             with torch.cuda.stream(self._comm_stream):
+                self._debug_delay()
                 dist.all_gather_into_tensor(full, mine, group=self.topology.data_parallel_group)
                 ev = torch.cuda.Event()
                 ev.record(self._comm_stream)

@@ -14,6 +14,7 @@ between resumes from the previous complete checkpoint.
 """
 from __future__ import annotations
 
+import copy
 import os
 import queue
 import threading
@@ -24,17 +25,23 @@ import torch
 
 
 def _snapshot(obj: Any) -> Any:
-    """Deep copy with every tensor moved to (unshared) host memory."""
+    """Deep copy with every tensor moved to (unshared) host memory.  Mappings become plain dicts (a ``defaultdict``
+    or other dict subclass cannot always be rebuilt from pairs, and ``torch.save`` needs no subclass), named tuples
+    keep their type, and mutable non-tensor leaves (sets, objects) are deep-copied so later training-state
+    mutation cannot leak into a queued file."""
     if isinstance(obj, torch.Tensor):
         t = obj.detach()
         return t.to("cpu", copy=True) if t.device.type != "cpu" else t.clone()
     if isinstance(obj, dict):
-        return type(obj)((k, _snapshot(v)) for k, v in obj.items())
+        return {k: _snapshot(v) for k, v in obj.items()}
     if isinstance(obj, list):
         return [_snapshot(v) for v in obj]
     if isinstance(obj, tuple):
-        return tuple(_snapshot(v) for v in obj)
-    return obj
+        items = [_snapshot(v) for v in obj]
+        return type(obj)(*items) if hasattr(obj, "_fields") else tuple(items)
+    if obj is None or isinstance(obj, (bool, int, float, complex, str, bytes, Path)):
+        return obj
+    return copy.deepcopy(obj)
 
 
 class CheckpointWriter:

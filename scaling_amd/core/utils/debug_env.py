@@ -38,6 +38,17 @@ DETERMINISTIC_ENV: Mapping[str, str] = {
 SINGLE_STREAM_ENV: Mapping[str, str] = {"SCALING_AMD_SINGLE_STREAM": "1"}
 
 
+# race check with a late communication stream: SCALING_AMD_COMM_DELAY_US=<us> enqueues a busy-wait kernel of that
+# length on the DP communication stream in front of every gradient reduce-scatter and parameter all-gather, so a
+# consumer that forgot to wait for the stream reads stale data with near certainty instead of by timing luck.
+# Results must stay bit-identical to the undelayed run (tests/test_gpu_rehearsal.py).
+def comm_delay_us() -> int:
+    try:
+        return max(0, int(os.environ.get("SCALING_AMD_COMM_DELAY_US", "0") or 0))
+    except ValueError:
+        return 0
+
+
 def side_streams_enabled() -> bool:
     return os.environ.get("SCALING_AMD_SINGLE_STREAM", "0") in ("", "0")
 

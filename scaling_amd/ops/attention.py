@@ -223,8 +223,11 @@ def flash_attention(
     if use_native(q):
         p_drop = float(dropout_p) if training else 0.0
         in_dtype = q.dtype
-        if in_dtype not in (torch.bfloat16, torch.float16):  # fp32 runs through the bf16 kernel
-            q, k, v = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
+        if in_dtype not in (torch.bfloat16, torch.float16):
+            # as flash-attn (the reference's kernel) does: the MFMA kernels are bf16/fp16 only, and silently
+            # computing an fp32 model's attention in bf16 would make an fp32 run useless as an fp32 oracle
+            raise TypeError(f"flash attention supports bfloat16 / float16 inputs, got {in_dtype}; "
+                            "use masked_softmax.kernel 'torch' for float32 models")
         cq = cu_seqlens_q.to(torch.int32)
         ck = cu_seqlens_k.to(torch.int32)
         if max_seqlen_q is None:

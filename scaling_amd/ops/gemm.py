@@ -43,10 +43,14 @@ GEMV_MAX_ROWS = 4
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear(x, w, b)``; decode-sized inputs (<= 4 rows) on the GEMV kernel."""
+    """``F.linear(x, w, b)``; decode-sized inputs (<= 4 rows) on the GEMV kernel.
+
+    The GEMV kernel is a raw op without autograd, so it only serves calls that build no graph (grad mode off, or
+    no operand requiring grad); a tiny training micro-batch through a tied head keeps ``F.linear``'s backward."""
     K = x.shape[-1]
     rows = x.numel() // K if K else 0
-    if 0 < rows <= GEMV_MAX_ROWS and use_native(x) and w.dim() == 2:
+    needs_graph = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or (b is not None and b.requires_grad))
+    if 0 < rows <= GEMV_MAX_ROWS and not needs_graph and use_native(x) and w.dim() == 2:
         x2 = x.reshape(rows, K)
         if ext().gemv_ok(x2, w) and (b is None or b.dtype == w.dtype):
             return ext().gemv(x2, w, b).reshape(*x.shape[:-1], w.shape[0])

@@ -8,6 +8,11 @@ slot capacity, or that are not a multiple of 16 bytes, return False and the call
 
 Opt-in for tensor parallelism with ``SCALING_AMD_CUSTOM_ALLREDUCE=1`` (``parallel.tp.raw_all_reduce``): the
 protocol is exercised by a 2-process test on one GPU; multi-GPU xGMI runs are not covered by the test-suite.
+
+Safety: enabling is a GROUP decision (every rank allocates / maps, then a MIN all-reduce of the per-rank success
+flag; all ranks use the path or none does), and a flag-wait timeout in the kernel poisons the output with NaN and
+sets the communicator's error word, which ``pending_error_words`` hands to the optimizer's per-step host read
+(``Optimizer._grad_stats``) so the step raises instead of training on garbage.
 """
 from __future__ import annotations
 
@@ -29,22 +34,49 @@ def enabled() -> bool:
 
 
 class OneShotAllReduce:
-    def __init__(self, group: Any, device: torch.device, capacity_bytes: int = 32 << 20) -> None:
+    def __init__(self, group: Any, device: torch.device, capacity_bytes: int = 32 << 20,
+                 max_spins: int = 1 << 26) -> None:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         assert 1 <= self.world <= 8, "one-shot all-reduce supports up to 8 ranks"
         self.device = device
         self.cap = int(capacity_bytes) // 256 * 256
-        dev = device.index if device.index is not None else torch.cuda.current_device()
-        self.own, handle = ext().ar_alloc(2 * self.cap + _FLAG_BYTES, dev)
-        info = (handle, socket.gethostname())
-        infos: list[Any] = [None] * self.world
-        dist.all_gather_object(infos, info, group=group)
-        self.single_node = len({h for _, h in infos}) == 1
-        self.bases = [self.own if i == self.rank else ext().ar_open(h, dev) for i, (h, _) in enumerate(infos)]
+        dev = device.index if device.index is not None else (torch.cuda.current_device() if device.type == "cuda" else 0)
+        self.own: Optional[int] = None
+        self.bases: list[int] = []
         self.epoch = 0
+        self.max_spins = int(max_spins)  # flag-wait bound per peer (~seconds at the default)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        handle: Optional[bytes] = None
+        ok = True
+        try:
+            self.own, handle = ext().ar_alloc(2 * self.cap + _FLAG_BYTES, dev)
+        except Exception:  # noqa: BLE001 - decided collectively below
+            ok = False
+        infos: list[Any] = [None] * self.world
+        dist.all_gather_object(infos, (handle, socket.gethostname()), group=group)  # every rank reaches this
+        self.single_node = len({h for _, h in infos}) == 1
+        opened: dict[int, int] = {}
+        if ok and self.single_node and all(h is not None for h, _ in infos):
+            try:
+                for i, (h, _) in enumerate(infos):
+                    if i != self.rank:
+                        opened[i] = ext().ar_open(h, dev)
+            except Exception:  # noqa: BLE001
+                ok = False
+        else:
+            ok = False
+        if not _group_all(ok, group, device):
+            for b in opened.values():
+                ext().ar_close(b)
+            if self.own is not None:
+                if device.type == "cuda":
+                    torch.cuda.synchronize(device)
+                ext().ar_free(self.own)
+            self.own = None
+            raise RuntimeError("one-shot all-reduce unavailable on at least one rank of the group")
+        self.bases = [self.own if i == self.rank else opened[i] for i in range(self.world)]
 
     def __call__(self, x: torch.Tensor) -> bool:
         if not (self.single_node and x.is_cuda and x.is_contiguous() and x.nbytes <= self.cap and x.nbytes % 16 == 0
@@ -52,7 +84,7 @@ class OneShotAllReduce:
             return False
         self.epoch += 1
         slot = (self.epoch & 1) * self.cap
-        ext().ar_allreduce(x, self.bases, self.rank, slot, 2 * self.cap, self.epoch, True, self.err)
+        ext().ar_allreduce(x, self.bases, self.rank, slot, 2 * self.cap, self.epoch, True, self.err, self.max_spins)
         return True
 
     def check(self) -> None:
@@ -67,17 +99,42 @@ class OneShotAllReduce:
             if i != self.rank:
                 ext().ar_close(b)
         dist.barrier(group=self.group)
-        ext().ar_free(self.own)
+        if self.own is not None:
+            ext().ar_free(self.own)
+        self.own = None
         self.bases = []
 
 
+def _group_all(ok: bool, group: Any, device: torch.device) -> bool:
+    """True iff `ok` holds on every rank of `group` (MIN all-reduce; the tensor lives where the backend wants it)."""
+    on_gpu = dist.get_backend(group) == "nccl"
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device if on_gpu else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(flag.item()) == 1)
+
+
 def for_group(group: Any, device: torch.device) -> Optional[OneShotAllReduce]:
-    """The group's communicator (created on first use, collectively), or None when disabled / not possible."""
+    """The group's communicator (created on first use, collectively), or None when disabled / not possible.
+
+    Every rank of the group must call this at the same point (it is reached from the same collective call site
+    on all ranks); the constructor's success is agreed on collectively, so either all ranks get a communicator or
+    all get None and stay on RCCL."""
     if not enabled() or device.type != "cuda":
         return None
     if group not in _REGISTRY:
         try:
             _REGISTRY[group] = OneShotAllReduce(group, device)
-        except Exception:  # noqa: BLE001 - IPC unavailable: stay on RCCL
+        except RuntimeError:  # agreed on by every rank: stay on RCCL everywhere
             _REGISTRY[group] = None
     return _REGISTRY[group]
+
+
+def pending_error_words() -> list[torch.Tensor]:
+    """Device error words of every live communicator (non-zero = a call timed out waiting for a peer)."""
+    return [ar.err for ar in _REGISTRY.values() if ar is not None]
+
+
+def reset_error_words() -> None:
+    for ar in _REGISTRY.values():
+        if ar is not None:
+            ar.err.zero_()

@@ -246,3 +246,24 @@ def test_attention_reference_mixed_local_global_heads_matches_two_calls():
     loc = attention_reference(q[:, :nl], kr[:, :nl], vr[:, :nl], cu, cu, 0.25, True, w)
     glob = attention_reference(q[:, nl:], kr[:, nl:], vr[:, nl:], cu, cu, 0.25, True, -1)
     torch.testing.assert_close(both, torch.cat([loc, glob], 1))
+
+
+def test_async_checkpoint_snapshot_handles_dict_subclasses_and_mutable_leaves():
+    """The async writer's host snapshot must accept what a synchronous torch.save accepts (a defaultdict in the
+    state) and must not share mutable leaves with the live training state."""
+    import collections
+
+    import torch
+
+    from scaling_amd.core.utils.checkpoint_writer import _snapshot
+
+    d = collections.defaultdict(list)
+    d["a"].append(torch.ones(2))
+    live_set = {1, 2}
+    nt = collections.namedtuple("NT", "x y")(torch.zeros(1), 3)
+    snap = _snapshot({"d": d, "s": live_set, "nt": nt})
+    live_set.add(3)
+    d["a"][0].add_(5)
+    assert snap["s"] == {1, 2}
+    assert torch.equal(snap["d"]["a"][0], torch.ones(2))
+    assert type(snap["nt"]).__name__ == "NT" and snap["nt"].y == 3

@@ -76,3 +76,25 @@ def test_oneshot_allreduce_two_processes_one_gpu():
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     assert all(run_distributed(_two_procs_one_gpu, 2, timeout=120).values())
+
+
+def test_oneshot_timeout_poisons_output_and_sets_error():
+    """A peer that never arrives: the bounded flag wait gives up, the output is NaN (not a sum of stale slots) and
+    the error word is set (the optimizer raises on it at its per-step read)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    cap = 1 << 16
+    e = _ext()
+    own, other = e.ar_alloc(2 * cap + 256, 0)[0], e.ar_alloc(2 * cap + 256, 0)[0]
+    try:
+        x = torch.randn(4096, device="cuda", dtype=torch.bfloat16)
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        # rank 0 of a 2-rank group whose rank 1 ("other") never signals
+        e.ar_allreduce(x, [own, other], 0, 0, 2 * cap, 7, True, err, 1 << 10)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 1
+        assert torch.isnan(x.float()).all()
+    finally:
+        torch.cuda.synchronize()
+        e.ar_free(own)
+        e.ar_free(other)

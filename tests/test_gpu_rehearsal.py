@@ -99,6 +99,8 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         (["--gpus", "1", "--backend", "auto"], {}),                            # overlapped step on its side stream
         (["--gpus", "1", "--backend", "auto"], {"SCALING_AMD_WGRAD_STREAM": "1"}),  # + weight-gradient stream
         (["--gpus", "2"], {}),                                                 # DP comm stream
+        (["--gpus", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),              # ... running 1 ms late per collective
+        (["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),
         (["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {}),
     ],
 )
@@ -144,3 +146,53 @@ def test_rehearsal_layout_change_resume_gpu(tmp_path, before, after):
     a = [m["training/loss"] for m in full][-4:]
     b = [m["training/loss"] for m in resumed]
     assert len(b) == 4 and all(abs(x - y) / x < 0.15 for x, y in zip(a, b)), (a, b)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("mp,pp,world,initial_scale", [(1, 1, 1, 16.0), (2, 1, 2, 16.0), (1, 1, 2, 2.0 ** 40)])
+def test_rehearsal_fp16_loss_scaling_resume_bit_exact_gpu(tmp_path, mp, pp, world, initial_scale):
+    """fp16 + dynamic loss scaling on the GPU path (flash attention in fp16, fp16 weight gradients through the
+    hipBLASLt fallback of the bf16-only hand-written wgrad kernel, fused fp16 AdamW / grad-norm): trains, skips the
+    overflowing steps of a 2^40 initial scale on every rank, and resumes bit-exactly from the step-6 checkpoint."""
+    import numpy as np
+
+    from tests.test_training import _config, _make_data, _run as _train
+
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, mp, pp, world, precision="float16", masked_softmax={"kernel": "flash_attention"},
+                  hidden_size=128, sequence_length=128)
+    cfg["optimizer"]["loss_scaler"] = {"enable": True, "initial_scale": initial_scale, "window": 3, "hysteresis": 1}
+    cfg["topology"]["backend"] = "gloo"
+    cfg["topology"]["gloo_on_gpu"] = True
+    full = _train(tmp_path, cfg, world, "full")
+    assert len(full) == 10 and all(np.isfinite(m["training/loss"]) for m in full)
+    scales = [m["training/current_loss_scale"] for m in full]
+    if initial_scale > 1e9:
+        assert any(m["training/overflow"] for m in full) and scales[-1] < initial_scale
+    else:
+        assert max(scales) > initial_scale
+    cfg["trainer"]["assert_checkpoint_loaded"] = True
+    resumed = _train(tmp_path, cfg, world, "resumed")
+    assert [m["training/loss"] for m in resumed] == [m["training/loss"] for m in full[-4:]]
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("kernel", ["torch", "flash_attention"])
+def test_deterministic_torch_training_gpu(tmp_path, kernel):
+    """``training.use_deterministic_torch_algorithms: true`` (reference tests/transformer/test_training.py:845-862)
+    trains on the GPU with every torch op passing the deterministic-algorithms check (the dense mask builder uses
+    a sorted search, not a scatter-add), and two runs give bit-identical losses."""
+    import numpy as np
+
+    from tests.test_training import _config, _make_data, _run as _train
+
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, 1, 1, 1, precision="bfloat16", masked_softmax={"kernel": kernel},
+                  hidden_size=128, sequence_length=128)
+    cfg["training"]["use_deterministic_torch_algorithms"] = True
+    cfg["trainer"]["save_dir"] = None
+    cfg["trainer"]["load_dir"] = None
+    a = _train(tmp_path, cfg, 1, "det_a")
+    b = _train(tmp_path, cfg, 1, "det_b")
+    assert len(a) == 10 and all(np.isfinite(m["training/loss"]) for m in a)
+    assert [m["training/loss"] for m in a] == [m["training/loss"] for m in b]

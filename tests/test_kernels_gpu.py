@@ -373,6 +373,14 @@ def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0,
         assert err / scl < 3e-2, (err, scl)
 
 
+def test_flash_attention_rejects_fp32():
+    """fp32 q/k/v are refused (flash-attn's contract) instead of being computed in bf16 behind the caller's back."""
+    q = torch.randn(64, 2, 64, device=DEV)
+    cu = torch.tensor([0, 64], dtype=torch.int32, device=DEV)
+    with pytest.raises(TypeError, match="float32"):
+        attention.flash_attention(q, q, q, cu, cu, 64, 64, 0.125, True, None)
+
+
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_basic(D, causal):
@@ -727,3 +735,24 @@ def test_norm_decode_rows_kernel(layer, rows, H):
            else norm.rms_norm_reference(xr2, wr, 1e-5))
     (gr,) = torch.autograd.grad(yr3, xr2, g.float())
     torch.testing.assert_close(gx.float(), gr, atol=4e-2, rtol=4e-2)
+
+
+@pytest.mark.parametrize("rows", [1, 2, 4])
+def test_small_linear_keeps_autograd(rows):
+    """ops.gemm.linear sends <= 4 rows to the (autograd-free) GEMV kernel only when no graph is needed: a tied-head
+    style call on a tiny training micro-batch must still produce gradients for the input and the weight."""
+    from scaling_amd.ops import gemm
+
+    torch.manual_seed(0)
+    w = torch.randn(256, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(rows, 128, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = gemm.linear(x, w)
+    assert y.grad_fn is not None
+    y.float().sum().backward()
+    wr = w.detach().float().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    torch.nn.functional.linear(xr, wr).sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.3, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.1, rtol=2e-2)
+    with torch.no_grad():  # inference keeps the GEMV path
+        torch.testing.assert_close(gemm.linear(x, w).float(), xr.detach() @ wr.detach().t(), atol=0.3, rtol=2e-2)

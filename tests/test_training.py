@@ -164,3 +164,16 @@ def test_bf16_gradient_reduction_tracks_fp32(tmp_path):
     assert a[0] == b[0]
     assert not np.array_equal(a, b)  # the bf16 reduction path ran (different rounding from step 2 on)
     assert np.max(np.abs(a - b) / np.abs(a)) < 2e-2, (a, b)
+
+
+def test_deterministic_torch_training_cpu(tmp_path):
+    """``training.use_deterministic_torch_algorithms: true`` on the CPU path: every op passes torch's check and two
+    runs are bit-identical (reference tests/transformer/test_training.py:845-862)."""
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, 1, 1, 1)
+    cfg["training"]["use_deterministic_torch_algorithms"] = True
+    cfg["trainer"]["save_dir"] = None
+    cfg["trainer"]["load_dir"] = None
+    a = _run(tmp_path, cfg, 1, "det_a")
+    b = _run(tmp_path, cfg, 1, "det_b")
+    assert [m["training/loss"] for m in a] == [m["training/loss"] for m in b]
