@@ -62,6 +62,8 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--activation-checkpointing", type=str, default="disabled",
                    choices=["disabled", "every_layer", "every_pipe_stage"])
     p.add_argument("--sequence-parallel", action="store_true")
+    p.add_argument("--tp-comm-chunks", type=int, default=1,
+                   help="row-parallel GEMM + TP all-reduce / SP reduce-scatter in this many overlapped token pieces")
     p.add_argument("--zero", type=int, default=1)
     p.add_argument("--overlap-step", type=int, default=1,
                    help="run the optimizer update on a side stream, overlapped with the next forward (1) or inline (0)")
@@ -188,6 +190,7 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
         "model_parallel_size": a.tp, "pipe_parallel_size": a.pp, "data_parallel_size": dp,
         "micro_batch_size": a.micro_batch, "gradient_accumulation_steps": a.grad_acc,
         "activation_checkpointing_type": a.activation_checkpointing, "sequence_parallel": a.sequence_parallel,
+        "tensor_parallel_comm_chunks": a.tp_comm_chunks,
     }
     if a.backend in ("gloo", "gloo-gpu"):
         topo["backend"] = "gloo"
@@ -240,6 +243,7 @@ def _worker(a: argparse.Namespace) -> None:
     from scaling_amd.transformer.data.text_dataset import TextDataset
     from scaling_amd.transformer.model import init_model, init_optimizer
     from scaling_amd.transformer.model.model import loss_function, metrics_aggregation_fn
+    from scaling_amd.transformer.utils.comm_estimate import comm_volume_estimate
     from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
 
     gpu = a.backend != "gloo"
@@ -300,6 +304,7 @@ def _worker(a: argparse.Namespace) -> None:
     dist.all_reduce(agree_t, op=dist.ReduceOp.MIN)
     dp_agree = bool(agree_t.item() == 1.0)
     _, unique_params = model.get_params_count()
+    local_params = sum(p.numel() for p in model.parameters() if p.requires_grad)
 
     gbs = config.topology.global_batch_size
     tokens = gbs * a.seq_len * a.steps
@@ -346,6 +351,13 @@ def _worker(a: argparse.Namespace) -> None:
                 "dp_param_checksum_agree": dp_agree,
                 "param_checksum": [float(v) for v in ck.tolist()],
                 "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if dev.type == "cuda" else None,
+                "tp_comm_chunks": a.tp_comm_chunks,
+                # what this layout must move per step and rank (first-order xGMI time, no overlap): a reading aid for
+                # multi-GPU results (scaling_amd/transformer/utils/comm_estimate.py)
+                "comm_estimate": comm_volume_estimate(
+                    hidden_size=arch["hidden_size"], num_layers=arch["num_layers"], seq_len=a.seq_len,
+                    micro_batch=a.micro_batch, grad_acc=a.grad_acc, tp=a.tp, pp=a.pp, dp=dp,
+                    params_per_rank=local_params, precision=a.precision),
             },
         }
         if a.profile_json:

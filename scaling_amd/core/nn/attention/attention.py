@@ -551,6 +551,9 @@ class ParallelSelfAttention(torch.nn.Module):
             if not (mp == 1 and self._lora_gemm_accumulates(mod)):
                 dense_lora = mod(all_concat(hidden, dim=-1, topology=self.topology))
                 mod = None
+        sp = self.topology is not None and self.topology.config.sequence_parallel
+        if sp and mod is None and dense_lora is None:  # reduce-scatter fused with (overlapped by) the dense GEMM
+            return self.dense.forward_sequence_parallel(hidden)
         out = self.dense(hidden)
         if mod is not None and out._base is None:  # up-projection GEMM accumulates into the dense output
             h = torch.nn.functional.linear(hidden.reshape(-1, hidden.shape[-1]), mod.dense_in.weight.to(hidden.dtype))

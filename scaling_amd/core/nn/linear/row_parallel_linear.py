@@ -10,8 +10,9 @@ import torch
 
 from ...topology import Topology
 from ..parameter_meta import CoreParameterMeta
-from .utils import all_reduce, all_shard, get_device
+from .utils import all_reduce, all_reduce_scatter_to_sequence_parallel, all_shard, get_device
 from .main_grad import linear as main_grad_linear
+from .tp_overlap import chunked_supported, row_parallel_chunked
 
 
 class RowParallelLinear(torch.nn.Module):
@@ -59,11 +60,30 @@ class RowParallelLinear(torch.nn.Module):
     def bias_param(self) -> Optional[torch.Tensor]:
         return getattr(self, self.bias_name) if self.bias_name is not None else None
 
+    def _chunks(self) -> int:
+        if self.topology is None or self.model_parallel_size == 1:
+            return 1
+        return int(getattr(self.topology.config, "tensor_parallel_comm_chunks", 1))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not self.parallel_input and self.topology is not None:
             x = all_shard(x, dim=-1, topology=self.topology)
-        out = main_grad_linear(x, self.weight)
-        if not self.parallel_output and self.topology is not None:
-            out = all_reduce(out, topology=self.topology)
+        reduce = not self.parallel_output and self.topology is not None
+        if reduce and chunked_supported(x, self.model_parallel_size, self._chunks(), False):
+            out = row_parallel_chunked(x, self.weight, self.topology, False, self._chunks())
+        else:
+            out = main_grad_linear(x, self.weight)
+            if reduce:
+                out = all_reduce(out, topology=self.topology)
         b = self.bias_param
         return out if b is None else out + b
+
+    def forward_sequence_parallel(self, x: torch.Tensor) -> torch.Tensor:
+        """``reduce_scatter_to_sequence_parallel(self(x))`` for a ``parallel_output`` layer (attention dense / MLP
+        dense_out under sequence parallelism), with the reduce-scatter overlapped piecewise with the GEMM when
+        ``topology.tensor_parallel_comm_chunks > 1`` (bias-free layers; a bias keeps the reference's order)."""
+        assert self.parallel_output and self.topology is not None
+        if (self.parallel_input and self.bias_param is None
+                and chunked_supported(x, self.model_parallel_size, self._chunks(), True)):
+            return row_parallel_chunked(x, self.weight, self.topology, True, self._chunks())
+        return all_reduce_scatter_to_sequence_parallel(self(x), self.topology)

@@ -15,7 +15,6 @@ from ..topology import Topology
 from .activation_function import ActivationFunction, get_activation_function
 from .linear import ColumnParallelLinear, RowParallelLinear
 from .linear.fused import fused_column_linear
-from .linear.utils import all_reduce_scatter_to_sequence_parallel
 
 
 def _intermediate(io_features: int, factor: float) -> int:
@@ -51,10 +50,10 @@ class ParallelMLP(torch.nn.Module):
         self.topology = topology
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.dense_out(self.activation_function(self.dense_in(x)))
+        h = self.activation_function(self.dense_in(x))
         if self.topology is not None and self.topology.config.sequence_parallel:
-            x = all_reduce_scatter_to_sequence_parallel(x, self.topology)
-        return x
+            return self.dense_out.forward_sequence_parallel(h)
+        return self.dense_out(h)
 
 
 class ParallelSwiGLUMLP(torch.nn.Module):
@@ -84,7 +83,6 @@ class ParallelSwiGLUMLP(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         z = fused_column_linear(x, [self.dense_in, self.siglu_weight], self.topology)
         h = swiglu_ops.swiglu_fused(z)
-        out = self.dense_out(h)
         if self.topology is not None and self.topology.config.sequence_parallel:
-            out = all_reduce_scatter_to_sequence_parallel(out, self.topology)
-        return out
+            return self.dense_out.forward_sequence_parallel(h)
+        return self.dense_out(h)

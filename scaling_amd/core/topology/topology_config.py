@@ -95,6 +95,14 @@ class TopologyConfig(BaseConfig):
         "visible devices, so several ranks may share one GPU, which RCCL refuses); exercises the GPU-side "
         "multi-rank paths (streams, events, kernels) on a 1-GPU box",
     )
+    tensor_parallel_comm_chunks: int = Field(
+        1,
+        description="row-parallel outputs (attention dense, MLP dense_out) are computed in this many token chunks "
+        "and the TP all-reduce (or sequence-parallel reduce-scatter) of chunk i runs on a communication stream "
+        "while chunk i+1 is multiplied; 1 = one GEMM then one collective (the reference's order)",
+        ge=1,
+        le=16,
+    )
 
     @model_validator(mode="before")
     @classmethod

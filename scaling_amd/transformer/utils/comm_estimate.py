@@ -1,0 +1,60 @@
+"""Per-step communication volume of a training layout (bytes each rank sends), and a first-order time estimate
+on MI355X xGMI, so a multi-GPU run can be read against what its layout must move.
+
+Model (one data-parallel replica processes ``micro_batch x grad_acc`` sequences of ``s`` tokens per step;
+``M = micro_batch * s`` tokens per micro-batch; activations in the model dtype, ``h`` = hidden size):
+
+* tensor parallel (``t > 1``), per layer and micro-batch: two row-parallel output reductions in the forward
+  (attention dense, MLP out) and two column-parallel input-gradient reductions in the backward, each an
+  all-reduce of ``[M, h]`` -- or, with sequence parallelism, a reduce-scatter + all-gather pair of the same
+  total -- at ``2 (t-1)/t x M h`` elements sent per rank (ring); plus the embedding's forward all-reduce;
+* pipeline parallel (``p > 1``), per micro-batch: the ``[M, h]`` activation forward and its gradient backward
+  across each stage boundary a rank owns (at most one of each direction per rank);
+* data parallel (``d > 1``, ZeRO-1 as implemented): reduce-scatter of the fp32 (or bf16, ``grad_reduce_dtype``)
+  gradient buckets and all-gather of the updated parameters, ``(d-1)/d`` of the rank's parameter shard each.
+
+Time: TP collectives of a TP group of 2 ride one xGMI link (~153 GB/s per direction, MI355X_MICROARCH.md);
+larger TP groups and DP rings are spread over ``min(group-1, 7)`` links by RCCL's multi-ring schedule.  The
+estimate assumes ``link_efficiency`` of that peak and no overlap; it is a reading aid, not a prediction.
+"""
+from __future__ import annotations
+
+from typing import Any
+
+XGMI_LINK_BYTES_PER_S = 153e9
+XGMI_LINKS_PER_GPU = 7
+
+
+def _dtype_bytes(precision: str) -> int:
+    return 4 if precision in ("float32", "fp32") else 2
+
+
+def comm_volume_estimate(*, hidden_size: int, num_layers: int, seq_len: int, micro_batch: int, grad_acc: int,
+                         tp: int, pp: int, dp: int, params_per_rank: int, precision: str = "bfloat16",
+                         grad_reduce_bytes: int = 4, link_efficiency: float = 0.7) -> dict[str, Any]:
+    act = _dtype_bytes(precision)
+    M = micro_batch * seq_len
+    ring = lambda n: 2.0 * (n - 1) / n if n > 1 else 0.0  # noqa: E731 - all-reduce bytes factor per rank
+    layers_here = num_layers / pp
+    tp_bytes = 0.0
+    if tp > 1:
+        per_mb = (4 * layers_here + 1) * ring(tp) * M * hidden_size * act  # + 1: embedding (first stage)
+        tp_bytes = per_mb * grad_acc
+    pp_bytes = 2.0 * M * hidden_size * act * grad_acc if pp > 1 else 0.0
+    dp_bytes = 0.0
+    if dp > 1:
+        frac = (dp - 1) / dp
+        dp_bytes = frac * params_per_rank * grad_reduce_bytes + frac * params_per_rank * act
+    eff_link = XGMI_LINK_BYTES_PER_S * link_efficiency
+
+    def t_ms(nbytes: float, group: int) -> float:
+        if nbytes == 0.0:
+            return 0.0
+        links = min(max(group - 1, 1), XGMI_LINKS_PER_GPU)
+        return 1e3 * nbytes / (eff_link * links)
+
+    return {
+        "tp_bytes": int(tp_bytes), "pp_bytes": int(pp_bytes), "dp_bytes": int(dp_bytes),
+        "tp_ms": round(t_ms(tp_bytes, tp), 2), "pp_ms": round(t_ms(pp_bytes, 2), 2), "dp_ms": round(t_ms(dp_bytes, dp), 2),
+        "assumptions": f"xGMI {XGMI_LINK_BYTES_PER_S / 1e9:.0f} GB/s/link x {link_efficiency}, no overlap",
+    }

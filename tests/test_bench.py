@@ -63,3 +63,19 @@ def test_bench_launcher_fail_fast():
     assert "rank 1 exited with 3" in r.stderr
     assert _json_lines(r.stdout) == []
     assert time.time() - t0 < 120
+
+
+@pytest.mark.parametrize("sp", [False, True])
+def test_bench_tp_comm_chunks_gloo(sp):
+    """TP2 (optionally + sequence parallel) with the row-parallel output collectives in 2 overlapped pieces gives the
+    loss of the one-piece run; the JSON carries the layout's communication estimate."""
+    extra = ["--sequence-parallel"] if sp else []
+    losses = {}
+    for c in ("1", "2"):
+        r = _run(["--gpus", "2", "--tp", "2", "--tp-comm-chunks", c, *extra, *TINY])
+        assert r.returncode == 0, r.stderr[-4000:]
+        res = _json_lines(r.stdout)[0]
+        losses[c] = res["config"]["loss"]
+        est = res["config"]["comm_estimate"]
+        assert est["tp_bytes"] > 0 and est["dp_bytes"] == 0 and est["pp_bytes"] == 0
+    assert losses["2"] == pytest.approx(losses["1"], rel=1e-5)

@@ -62,13 +62,18 @@ def test_rehearsal_tp_loss_matches_single_rank():
             "--steps", "2", "--warmup", "0"]
     losses = {}
     for tag, args in [("tp1", ["--gpus", "1"]), ("tp2", ["--gpus", "2", "--tp", "2"]),
-                      ("tp2_sp", ["--gpus", "2", "--tp", "2", "--sequence-parallel"])]:
+                      ("tp2_sp", ["--gpus", "2", "--tp", "2", "--sequence-parallel"]),
+                      # row-parallel GEMM + collective in 4 pieces overlapped on the TP communication stream
+                      ("tp2_chunks", ["--gpus", "2", "--tp", "2", "--tp-comm-chunks", "4"]),
+                      ("tp2_sp_chunks", ["--gpus", "2", "--tp", "2", "--sequence-parallel", "--tp-comm-chunks", "4"])]:
         r = _run([*args, *base], timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
         losses[tag] = _json_lines(r.stdout)[0]["config"]["loss"]
     assert all(math.isfinite(v) for v in losses.values()), losses
-    for tag in ("tp2", "tp2_sp"):
+    for tag in ("tp2", "tp2_sp", "tp2_chunks", "tp2_sp_chunks"):
         assert losses[tag] == pytest.approx(losses["tp1"], rel=2e-2), losses
+    assert losses["tp2_chunks"] == pytest.approx(losses["tp2"], rel=2e-3), losses
+    assert losses["tp2_sp_chunks"] == pytest.approx(losses["tp2_sp"], rel=2e-3), losses
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")

@@ -87,3 +87,37 @@ def _case():
 
 def test_tp_input_grad_allreduce_overlaps_wgrad():
     assert all(run_distributed(_case, 2).values())
+
+
+def _row_chunked_case(sp: bool, chunks: int):
+    """RowParallelLinear with ``tensor_parallel_comm_chunks``: the piecewise GEMM + all-reduce (or SP
+    reduce-scatter into the reference's flat token partition) equals the one-GEMM-then-collective path, forward
+    and backward (input gradient and weight gradient)."""
+    from scaling_amd.core.nn.linear import RowParallelLinear
+
+    topo = make_topology(model_parallel_size=2, sequence_parallel=sp)
+    rank = topo.model_parallel_rank
+    m = RowParallelLinear(32, 24, bias=False, topology=topo, parallel_input=True, parallel_output=sp)
+    torch.manual_seed(7 + rank)
+    with torch.no_grad():
+        m.weight.normal_()
+    x = torch.randn(4, 16, 16, requires_grad=True)  # [b, s, in/tp]: this rank's input shard
+    outs = {}
+    for c in (1, chunks):
+        object.__setattr__(topo.config, "tensor_parallel_comm_chunks", c)  # frozen config: test-only override
+        x.grad = None
+        m.weight.grad = None
+        y = m.forward_sequence_parallel(x) if sp else m(x)
+        torch.manual_seed(99 + rank)
+        g = torch.randn_like(y)
+        (y * g).sum().backward()
+        outs[c] = (y.detach().clone(), x.grad.clone(), m.weight.grad.clone())
+    for a, b in zip(outs[1], outs[chunks]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    assert outs[1][0].shape == ((4, 8, 24) if sp else (4, 16, 24))
+    return True
+
+
+@pytest.mark.parametrize("sp,chunks", [(False, 2), (False, 4), (True, 2), (True, 4)])
+def test_row_parallel_chunked_matches_unchunked(sp, chunks):
+    assert all(run_distributed(_row_chunked_case, 2, sp=sp, chunks=chunks).values())

@@ -168,3 +168,25 @@ def test_llama2_7b_example_config_matches_bench_architecture():
             continue
         assert got == v, (k, got, v)
     assert cfg.topology.micro_batch_size * cfg.topology.gradient_accumulation_steps == 8
+
+
+def test_comm_volume_estimate_by_layout():
+    """Hand-computed volumes: TP2 (4 all-reduces of [M, h] per layer + the embedding's), PP2 boundary
+    activations, DP ZeRO-1 reduce-scatter (fp32) + all-gather (bf16) of the rank's shard."""
+    from scaling_amd.transformer.utils.comm_estimate import comm_volume_estimate
+
+    h, L, s, mb, acc = 4096, 32, 4096, 2, 4
+    M = mb * s
+    e = comm_volume_estimate(hidden_size=h, num_layers=L, seq_len=s, micro_batch=mb, grad_acc=acc, tp=2, pp=1, dp=4,
+                             params_per_rank=3_000_000_000)
+    assert e["tp_bytes"] == int((4 * 32 + 1) * 1.0 * M * h * 2 * acc)
+    assert e["pp_bytes"] == 0
+    assert e["dp_bytes"] == int(0.75 * 3e9 * 4 + 0.75 * 3e9 * 2)
+    e2 = comm_volume_estimate(hidden_size=h, num_layers=L, seq_len=s, micro_batch=mb, grad_acc=acc, tp=2, pp=2, dp=2,
+                              params_per_rank=1_500_000_000)
+    assert e2["tp_bytes"] == int((4 * 16 + 1) * 1.0 * M * h * 2 * acc)
+    assert e2["pp_bytes"] == 2 * M * h * 2 * acc
+    assert e2["dp_ms"] > 0 and e2["tp_ms"] > 0
+    e1 = comm_volume_estimate(hidden_size=h, num_layers=L, seq_len=s, micro_batch=8, grad_acc=1, tp=1, pp=1, dp=1,
+                              params_per_rank=6_000_000_000)
+    assert (e1["tp_bytes"], e1["pp_bytes"], e1["dp_bytes"]) == (0, 0, 0)
