@@ -337,6 +337,28 @@ at::Tensor gemv(const at::Tensor& x, const at::Tensor& W, c10::optional<at::Tens
                     (int)K, cur_stream());
     return y;
 }
+// decode epilogues: y = rnd(x W^T) + res  (res [M, N]) ...
+at::Tensor gemv_residual(const at::Tensor& x, const at::Tensor& W, const at::Tensor& res) {
+    TORCH_CHECK(gemv_ok(x, W), "gemv_residual: unsupported operands");
+    const int64_t M = x.size(0), N = W.size(0), K = W.size(1);
+    TORCH_CHECK(res.is_cuda() && res.dim() == 2 && res.size(0) == M && res.size(1) == N && res.stride(1) == 1 &&
+                    res.scalar_type() == x.scalar_type(), "gemv_residual: res must be [M, N] of the input dtype");
+    const at::DeviceGuard g(x.device());
+    auto y = at::empty({M, N}, x.options());
+    sa_launch::gemv(dt(x), (int)M, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), nullptr, y.data_ptr(), N, (int)N,
+                    (int)K, cur_stream(), 1, res.data_ptr(), res.stride(0));
+    return y;
+}
+// ... and SwiGLU over W = [gate; up] ([2F, K]): y[:, n] = silu(x W_gate^T)[n] * (x W_up^T)[n], rounded as gemv + swiglu
+at::Tensor gemv_swiglu(const at::Tensor& x, const at::Tensor& W) {
+    TORCH_CHECK(gemv_ok(x, W) && W.size(0) % 2 == 0, "gemv_swiglu: unsupported operands");
+    const int64_t M = x.size(0), F = W.size(0) / 2, K = W.size(1);
+    const at::DeviceGuard g(x.device());
+    auto y = at::empty({M, F}, x.options());
+    sa_launch::gemv(dt(x), (int)M, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), nullptr, y.data_ptr(), F, (int)F,
+                    (int)K, cur_stream(), 2, nullptr, 0);
+    return y;
+}
 
 // ------------------------------------------------------------------ GEMM (weight gradient)
 // C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
@@ -587,6 +609,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("transpose2d", &transpose2d, "x^T (contiguous) for 2-byte 2-D matrices");
     m.def("gemv_ok", &gemv_ok, "whether gemv supports these operands");
     m.def("gemv", &gemv, "y = x W^T (+ b) for at most 4 rows of x (decode-time linear layers)", py::arg("x"), py::arg("W"), py::arg("bias") = py::none());
+    m.def("gemv_residual", &gemv_residual, "y = x W^T + res for at most 4 rows (decode MLP-out + residual)");
+    m.def("gemv_swiglu", &gemv_swiglu, "y = silu(x Wg^T) * (x Wu^T) for W = [Wg; Wu], at most 4 rows (decode)");
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
     m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());

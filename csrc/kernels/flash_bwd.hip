@@ -191,12 +191,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 8 * g + 4 * h);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[4 * g + j] = fast_exp2(__builtin_fmaf(s[4 * g + j], c2, -l4[j]));
+        }
+        if (need_mask) {  // boundary tiles only: a real (wave-uniform) branch, not per-element selects every tile
+            mask_fence();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = (crow(r) >= mlo && crow(r) <= mhi) ? s[r] : 0.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
             const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + 8 * g + 4 * h);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = 4 * g + j;
-                float p = fast_exp2(__builtin_fmaf(s[r], c2, -l4[j]));
-                if (need_mask) p = (crow(r) >= mlo && crow(r) <= mhi) ? p : 0.f;
+                const float p = s[r];
                 if constexpr (DROP) {  // dV sees the dropped P; dS = P (Z dP / (1-p) - delta)
                     const bool keep = drop_keep(drop_row(hs, q0s + qt + 4 * h + crow(r)), k0s + mykey, a.drop_thr);
                     s[r] = keep ? p * a.rp_drop : 0.f;

@@ -404,7 +404,8 @@ class ParallelSelfAttention(torch.nn.Module):
             max_seq_length if max_seq_length is not None else s, self.scaling_factor, self.causal,
             self.local_attention_window_size if nl > 0 else None,
             dropout_p=self.dropout_attention_probs if self.training else 0.0,
-            local_heads=self.num_local_attention_heads_per_partition if nl > 0 else None)
+            local_heads=self.num_local_attention_heads_per_partition if nl > 0 else None,
+            deterministic=self.masked_softmax_config.deterministic_flash_attn_bwd)
 
     def _lora_gemm_accumulates(self, m: torch.nn.Module) -> bool:
         """An adapter whose up-projection can accumulate into the base output (no biases, no active dropout)."""
@@ -520,7 +521,7 @@ class ParallelSelfAttention(torch.nn.Module):
             common = dict(
                 cu_seqlens_q=cumulative_seq_lengths, cu_seqlens_k=cu_k, max_seqlen_q=max_q, max_seqlen_k=max_k,
                 softmax_scale=self.scaling_factor, causal=self.causal, dropout_p=self.dropout_attention_probs,
-                training=self.training,
+                training=self.training, deterministic=self.masked_softmax_config.deterministic_flash_attn_bwd,
             )
             # mixed local/global heads: ONE launch, the kernel picks the window per q head (heads [0, nl)
             # windowed) — no second launch, no repeat_kv (reference attention.py:619-667 runs two)

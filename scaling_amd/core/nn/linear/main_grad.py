@@ -159,6 +159,15 @@ def _rehome_adjacent(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
     return _adjacent(weights)
 
 
+def adjacent_weights(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
+    """Zero-copy ``[sum N, K]`` view over weights that share one input (q/k/v, gate/up), re-homing weights no
+    optimizer owns into one buffer on first use; None if they cannot be made adjacent."""
+    w = _adjacent(weights)
+    if w is None and len(weights) > 1:
+        w = _rehome_adjacent(weights)
+    return w
+
+
 def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]:
     if not all(getattr(w, "_sa_main_grad", False) and w.grad is not None for w in weights):
         return None

@@ -11,10 +11,12 @@ from typing import Callable, Optional
 import torch
 
 from ...ops import swiglu as swiglu_ops
+from ...ops._ext import ext, use_native
 from ..topology import Topology
 from .activation_function import ActivationFunction, get_activation_function
 from .linear import ColumnParallelLinear, RowParallelLinear
 from .linear.fused import fused_column_linear
+from .linear.main_grad import adjacent_weights
 
 
 def _intermediate(io_features: int, factor: float) -> int:
@@ -79,6 +81,30 @@ class ParallelSwiGLUMLP(torch.nn.Module):
             f, io_features, parallel_input=True,
             parallel_output=(topology.config.sequence_parallel if topology is not None else False), **kw
         )
+
+    def decode_forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> Optional[torch.Tensor]:
+        """``residual + self(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, TP 1, bias-free) as two
+        GEMV launches with fused epilogues -- gate/up GEMV + SwiGLU, down GEMV + residual add -- bit-identical to
+        the unfused GEMV / SwiGLU / add sequence; None when the fused path does not apply."""
+        K = x.shape[-1]
+        rows = x.numel() // K if K else 0
+        if not (0 < rows <= 4 and use_native(x) and residual.shape == x.shape[:-1] + (self.dense_out.out_features,)):
+            return None
+        if self.topology is not None and self.topology.config.model_parallel_size > 1:
+            return None
+        params = (self.dense_in.weight, self.siglu_weight.weight, self.dense_out.weight)
+        if torch.is_grad_enabled() and (x.requires_grad or residual.requires_grad or any(p.requires_grad for p in params)):
+            return None
+        if any(getattr(m, "bias_param", None) is not None for m in (self.dense_in, self.siglu_weight, self.dense_out)):
+            return None
+        w = adjacent_weights([self.dense_in.weight, self.siglu_weight.weight])
+        x2 = x.reshape(rows, K)
+        wo = self.dense_out.weight
+        if (w is None or not ext().gemv_ok(x2, w) or wo.dtype != w.dtype or wo.stride(1) != 1 or wo.stride(0) % 8
+                or wo.shape[1] != w.shape[0] // 2 or wo.shape[1] % 8 or wo.data_ptr() % 16):
+            return None
+        h = ext().gemv_swiglu(x2, w)
+        return ext().gemv_residual(h, self.dense_out.weight, residual.reshape(rows, -1)).view(residual.shape)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         z = fused_column_linear(x, [self.dense_in, self.siglu_weight], self.topology)

@@ -24,6 +24,9 @@ class PipePartitionMethod(Enum):
 class ActivationCheckpointingType(Enum):
     EVERY_PIPE_STAGE = "every_pipe_stage"
     EVERY_LAYER = "every_layer"
+    # MI355X addition: per-layer recompute that keeps each layer's flash-attention output + LSE, so the backward's
+    # recompute skips the attention forward (``ops.attention.AttentionStash``)
+    EVERY_LAYER_KEEP_ATTENTION = "every_layer_keep_attention"
     DISABLED = "disabled"
 
 

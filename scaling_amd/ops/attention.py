@@ -3,7 +3,10 @@
 Replaces the reference's CUDA ``flash_attn_varlen_func`` dependency (``attention.py:204-259``).
 Layout is token-major ``[T, heads, head_dim]`` with arbitrary token/head strides, so q/k/v can be
 strided views of the fused QKV projection (no ``rearrange`` copies, no ``repeat_kv``).
-Backward is deterministic (dK/dV and dQ each owned by one workgroup, no float atomics).
+Backward is deterministic (dK/dV and dQ each owned by one workgroup, no float atomics) for either value of
+``deterministic`` (``MaskedSoftmaxConfig.deterministic_flash_attn_bwd``): on MI355X an atomic-dQ backward is
+slower (its dQ adds alone are floored at 108.7 ms per 7B step by the ~1.3 TB/s float-atomic rate,
+``tools/atomic_dq_floor.hip``, vs 47 ms for the deterministic dQ pass).
 bf16 and fp16 operands run natively (fp32 inputs are computed in bf16).  Attention-probability dropout
 (reference ``flash_attn_varlen_func(dropout_p=...)``, ``attention.py:245-258``) is fused: the keep mask
 is a counter-based hash of (seed, q head, query token, key token) regenerated in the backward kernels,
@@ -11,8 +14,10 @@ so no mask is stored; :func:`dropout_keep_mask` is its exact PyTorch twin.
 """
 from __future__ import annotations
 
+import contextlib
 import math
-from typing import Any, Optional
+import threading
+from typing import Any, Iterator, Optional
 
 import torch
 
@@ -111,11 +116,53 @@ def attention_reference(q, k, v, cu_q, cu_k, scale, causal, window=-1, dropout_p
     return out
 
 
+class AttentionStash:
+    """Flash-attention outputs kept across an activation-checkpointed region (``activation_checkpointing_type:
+    every_layer_keep_attention``): the region's first forward records every flash call's output and log-sum-exp,
+    and the recompute in the backward replays them in call order instead of running the attention forward again
+    (everything else of the layer -- GEMMs, norms, RoPE -- is recomputed as usual).  Costs the attention output +
+    LSE per layer in memory; saves one flash forward per layer and step."""
+
+    def __init__(self) -> None:
+        self.items: list[Optional[tuple[torch.Tensor, torch.Tensor]]] = []
+        self.pos = 0
+
+
+_stash_state = threading.local()
+
+
+@contextlib.contextmanager
+def attention_stash(stash: Optional[AttentionStash], mode: str) -> Iterator[None]:
+    """Makes flash-attention calls inside the block record into (``mode='record'``) or replay from
+    (``mode='replay'``) ``stash``; ``stash=None`` is a no-op."""
+    prev = getattr(_stash_state, "cur", None)
+    _stash_state.cur = None if stash is None else (stash, mode)
+    try:
+        yield
+    finally:
+        _stash_state.cur = prev
+
+
+def _fa_fwd_stashed(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k):
+    cur = getattr(_stash_state, "cur", None)
+    if cur is not None and cur[1] == "replay":
+        stash = cur[0]
+        if stash.pos < len(stash.items) and stash.items[stash.pos] is not None:
+            o, lse = stash.items[stash.pos]  # type: ignore[misc]
+            stash.items[stash.pos] = None  # the replaying node's saved tensors hold them from here on
+            stash.pos += 1
+            return o.detach(), lse
+    o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
+    if cur is not None and cur[1] == "record":
+        cur[0].items.append((o.detach(), lse))
+    return o, lse
+
+
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def forward(ctx: Any, q, k, v, cu_q, cu_k, max_q, max_k, scale, causal, window, p_drop=0.0, seed=0,  # type: ignore[override]
                 local_heads=-1):
-        o, lse = ext().fa_fwd(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
+        o, lse = _fa_fwd_stashed(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
         ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
         ctx.cfg = (max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
@@ -151,7 +198,7 @@ class _RopeFlashAttn(torch.autograd.Function):
         qi, ki, vi = (_view(base, sp) for sp in specs)
         q = ext().rope(qi, cos, sin, pos, rot_dim, seq_len, interleaved, False)
         k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
-        o, lse = ext().fa_fwd(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
+        o, lse = _fa_fwd_stashed(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
         ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
         ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
@@ -174,7 +221,7 @@ def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v
                          sin: torch.Tensor, pos: Optional[torch.Tensor], rot_dim: int, seq_len: int, interleaved: bool,
                          cu_seqlens: torch.Tensor, max_seqlen: int, softmax_scale: float, causal: bool = True,
                          window: Optional[int] = None, dropout_p: float = 0.0,
-                         local_heads: Optional[int] = None) -> Optional[torch.Tensor]:
+                         local_heads: Optional[int] = None, deterministic: bool = True) -> Optional[torch.Tensor]:
     """Fused RoPE + flash attention for q/k/v that are views tiling ``base`` exactly (the QKV GEMM output).
 
     Returns None when the fused path does not apply (CPU tensors, layouts that do not tile ``base``); the
@@ -210,6 +257,7 @@ def flash_attention(
     dropout_p: float = 0.0,
     training: bool = False,
     local_heads: Optional[int] = None,
+    deterministic: bool = True,
 ) -> torch.Tensor:
     """q: [T, Hq, D]; k, v: [Tk, Hk, D] (unit last stride); cu_seqlens int32 [nseg+1].
 

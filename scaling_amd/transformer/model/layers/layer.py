@@ -111,7 +111,12 @@ class TransformerLayer(TransformerLayerBaseIO):
         )
 
     def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor) -> torch.Tensor:
-        out = self._dropout_add(self.dropout_mlp, self.mlp(normed), residual)
+        out = None
+        fused = getattr(self.mlp, "decode_forward_residual", None)
+        if fused is not None and (self.dropout_mlp.p == 0.0 or not self.training):
+            out = fused(normed, residual)  # decode-sized rows: GEMV epilogues (SwiGLU, residual add)
+        if out is None:
+            out = self._dropout_add(self.dropout_mlp, self.mlp(normed), residual)
         if hasattr(self, "mlp_adapter_name"):
             out = out + self.apply_adapter(out, self.mlp_adapter_name)
         return out

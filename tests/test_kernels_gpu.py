@@ -756,3 +756,26 @@ def test_small_linear_keeps_autograd(rows):
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.1, rtol=2e-2)
     with torch.no_grad():  # inference keeps the GEMV path
         torch.testing.assert_close(gemm.linear(x, w).float(), xr.detach() @ wr.detach().t(), atol=0.3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("rows", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemv_epilogues_bit_identical(rows, dtype):
+    """Decode GEMV epilogues: gate/up GEMV + SwiGLU and down GEMV + residual add in one launch each, bit-identical
+    to the unfused GEMV / SwiGLU kernel / torch add sequence (so cached decoding rounds like the eager path)."""
+    from scaling_amd.ops import swiglu
+
+    torch.manual_seed(rows)
+    F, K = 1376, 512
+    x = torch.randn(rows, K, device=DEV, dtype=dtype)
+    w = torch.randn(2 * F, K, device=DEV, dtype=dtype) / 16
+    wo = torch.randn(K, F, device=DEV, dtype=dtype) / 16
+    res = torch.randn(rows, K, device=DEV, dtype=dtype)
+    h_ref = swiglu.swiglu_fused(ext().gemv(x, w, None))
+    h = ext().gemv_swiglu(x, w)
+    assert torch.equal(h, h_ref)
+    ref = res + ext().gemv(h_ref, wo, None)
+    assert torch.equal(ext().gemv_residual(h, wo, res), ref)
+    # against fp32 math
+    hf = torch.nn.functional.silu(x.float() @ w[:F].float().t()) * (x.float() @ w[F:].float().t())
+    torch.testing.assert_close(h.float(), hf, atol=2e-2, rtol=2e-2)

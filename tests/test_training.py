@@ -177,3 +177,17 @@ def test_deterministic_torch_training_cpu(tmp_path):
     a = _run(tmp_path, cfg, 1, "det_a")
     b = _run(tmp_path, cfg, 1, "det_b")
     assert [m["training/loss"] for m in a] == [m["training/loss"] for m in b]
+
+
+@pytest.mark.parametrize("mp,pp,world", [(1, 1, 1), (2, 1, 2)])
+def test_keep_attention_checkpointing_matches_every_layer(tmp_path, mp, pp, world):
+    """``activation_checkpointing_type: every_layer_keep_attention`` trains exactly like ``every_layer`` (on CPU the
+    attention has no flash kernel to keep, so this pins the mode's plumbing; the GPU test pins the reuse)."""
+    _make_data(tmp_path / "data")
+    runs = {}
+    for ac in ("every_layer", "every_layer_keep_attention"):
+        cfg = _config(tmp_path, mp, pp, world, checkpointing=ac)
+        cfg["trainer"]["save_dir"] = None
+        cfg["trainer"]["load_dir"] = None
+        runs[ac] = [m["training/loss"] for m in _run(tmp_path, cfg, world, ac)]
+    assert runs["every_layer"] == runs["every_layer_keep_attention"]
