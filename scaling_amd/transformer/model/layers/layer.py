@@ -2,6 +2,7 @@
 block with residuals, dropouts under the TP-constant RNG, optional bottleneck adapters."""
 from __future__ import annotations
 
+import os
 from functools import partial
 from typing import Callable, Optional, Union
 
@@ -12,6 +13,9 @@ from ....ops.elementwise import dropout_add
 from ...context.config import MLPType, TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
 from .embedding import _device
+
+# decode-sized MLP blocks on the fused GEMV epilogues (SwiGLU, residual add); SCALING_AMD_DECODE_FUSED=0 for A/B
+_DECODE_FUSED = os.environ.get("SCALING_AMD_DECODE_FUSED", "1") != "0"
 
 
 class ZeroLayer(torch.nn.Module):
@@ -112,7 +116,7 @@ class TransformerLayer(TransformerLayerBaseIO):
 
     def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor) -> torch.Tensor:
         out = None
-        fused = getattr(self.mlp, "decode_forward_residual", None)
+        fused = getattr(self.mlp, "decode_forward_residual", None) if _DECODE_FUSED else None
         if fused is not None and (self.dropout_mlp.p == 0.0 or not self.training):
             out = fused(normed, residual)  # decode-sized rows: GEMV epilogues (SwiGLU, residual add)
         if out is None:

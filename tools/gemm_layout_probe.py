@@ -37,7 +37,12 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--tune", action="store_true", help="TunableOp-tune the hipBLASLt layouts first (as the bench does)")
     a = ap.parse_args()
+    if a.tune:
+        from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
+
+        print("gemm tuning:", enable_tuned_gemms("tune", "/tmp/gemm_layout_probe_tuned.csv"), flush=True)
     T = a.tokens
     out = {}
     tot = {"ours": 0.0, "tn": 0.0, "nn": 0.0, "nt": 0.0, "tr_dy": 0.0, "tr_x": 0.0}
