@@ -158,6 +158,29 @@ at::Tensor rope(const at::Tensor& x, const at::Tensor& cosb, const at::Tensor& s
     return out;
 }
 
+// graph decode: q = RoPE(q heads) (returned), K cache[pos] = RoPE(k heads), V cache[pos] = v heads, one launch;
+// qkv: the projection row [1, nq + 2 nkv, hd] (contiguous), caches [cap, nkv, hd] (contiguous), pos [1] int64
+c10::optional<at::Tensor> rope_kv_append(const at::Tensor& qkv, const at::Tensor& cosb, const at::Tensor& sinb,
+                                         const at::Tensor& pos, int64_t nq, int64_t nkv, int64_t rot_dim, bool interleaved,
+                                         at::Tensor kc, at::Tensor vc) {
+    check_cuda(qkv, "qkv");
+    const int64_t hd = qkv.size(-1);
+    if (!(qkv.is_contiguous() && qkv.numel() == (nq + 2 * nkv) * hd && kc.is_contiguous() && vc.is_contiguous() &&
+          kc.dim() == 3 && kc.size(1) == nkv && kc.size(2) == hd && vc.sizes() == kc.sizes() &&
+          kc.scalar_type() == qkv.scalar_type() && vc.scalar_type() == qkv.scalar_type() && pos.is_cuda() &&
+          pos.scalar_type() == at::kLong && pos.numel() == 1 && cosb.scalar_type() == at::kFloat &&
+          cosb.is_contiguous() && sinb.is_contiguous() && cosb.size(-1) == rot_dim / 2 &&
+          (uintptr_t)qkv.data_ptr() % 16 == 0 && (uintptr_t)kc.data_ptr() % 16 == 0 && (uintptr_t)vc.data_ptr() % 16 == 0))
+        return c10::nullopt;
+    const at::DeviceGuard g(qkv.device());
+    auto q = at::empty({1, nq, hd}, qkv.options());
+    if (!sa_launch::rope_kv_append(dt(qkv), interleaved, qkv.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                                   pos.data_ptr<int64_t>(), cosb.data_ptr<float>(), sinb.data_ptr<float>(), (int)nq,
+                                   (int)nkv, (int)hd, (int)rot_dim, cur_stream()))
+        return c10::nullopt;
+    return q;
+}
+
 // ------------------------------------------------------------------ cross entropy
 std::vector<at::Tensor> xent_stats(const at::Tensor& logits, const at::Tensor& target, int64_t v0) {
     check_cuda(logits, "logits");
@@ -614,6 +637,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
     m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());
+    m.def("rope_kv_append", &rope_kv_append, "graph decode: RoPE q, RoPE k into the K cache row, v into the V cache row");
     m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
     m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
     m.def("embed_fwd", &embed_fwd, "vocab-parallel embedding forward");

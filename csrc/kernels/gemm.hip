@@ -783,6 +783,165 @@ template __global__ void gemm_tn_il_kernel<false, true>(const u16* __restrict__,
                                                         int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
                                                         float* __restrict__, uint64_t* __restrict__);
 
+// ---------------------------------------------------------------------------------------------------------------
+// Variant 7: one wave per SIMD, register-staged.  The ping-pong kernels above pay for their LDS-DMA pieces in the
+// issue stream (~60 cycles per 1-KiB piece among MFMAs, 100-185 inside a read phase: MI355X_MICROARCH.md cycle
+// constants) and for 1.5 transposing LDS reads per MFMA at a 128x64 wave tile.  Here:
+//  * 4 waves x 128x128 (4 x 4 MFMA 32x32x16 tiles, 256 fp32 accumulators per lane in the unified register file):
+//    one transposing read per MFMA;
+//  * the next K-tile travels global -> VGPRs (16 B per lane per load, 64 staging VGPRs) and is written into the
+//    other LDS buffer with ds_write_b128 in the MFMA gaps of k-step 2; the global loads of the tile after it are
+//    issued right behind, so each load has about two K-tiles of latency cover;
+//  * one barrier per 64-deep K-tile, placed before the last k-step: right after it the wave reads the next tile's
+//    first fragments, whose latency hides behind the last k-step's 16 MFMAs.
+// LDS images and fragment reads are those of variant 2 (koff swizzle, frag_tr), written directly (no source
+// permutation: register staging writes any layout).
+template <bool BETA>
+__global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const u16* __restrict__ A, int lda,
+                                                            const u16* __restrict__ B, int ldb, u16* __restrict__ C,
+                                                            int ldc, int M, int N, int K, int full_blocks, int tail_split,
+                                                            float* __restrict__ ws) {
+    constexpr int BK = 64, IMG = BK * 256 * 2, STAGE = 2 * IMG;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tm = M / 256, tn = N / 256;
+    int v, k_lo = 0, nk = K / BK, unit = -1;
+    if ((int)blockIdx.x < full_blocks) {
+        v = xcd_remap(blockIdx.x, full_blocks);
+    } else {
+        unit = (int)blockIdx.x - full_blocks;
+        v = full_blocks + unit / tail_split;
+        nk /= tail_split;
+        k_lo = (unit % tail_split) * nk;
+    }
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    // staging: this wave moves image rows 16 wave + 2 i + (lane >> 5), i < 8, 16 B (8 columns) per lane
+    const int srow = 16 * wave + (lane >> 5), scol = 8 * (lane & 31);
+    // buffer loads: one 32-bit lane offset per operand, the row / K-tile steps in scalar offsets (64-bit per-load
+    // addresses would cost 32 VGPRs the staging registers need)
+    const __amdgpu_buffer_rsrc_t ra = fa::uniform_rsrc(A + (int64_t)k_lo * BK * lda + m0, (uint32_t)(nk * BK * lda * 2));
+    const __amdgpu_buffer_rsrc_t rb = fa::uniform_rsrc(B + (int64_t)k_lo * BK * ldb + n0, (uint32_t)(nk * BK * ldb * 2));
+    const int va = (srow * lda + scol) * 2, vb = (srow * ldb + scol) * 2;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 sa[8], sb[8];
+    auto load = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            sa[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, va, __builtin_amdgcn_readfirstlane((t * BK + 2 * i) * lda * 2), 0);
+            sb[i] = __builtin_amdgcn_raw_buffer_load_b128(rb, vb, __builtin_amdgcn_readfirstlane((t * BK + 2 * i) * ldb * 2), 0);
+        }
+    };
+    auto store = [&](char* st) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            *reinterpret_cast<u32x4*>(st + koff(srow + 2 * i, scol)) = sa[i];
+            *reinterpret_cast<u32x4*>(st + IMG + koff(srow + 2 * i, scol)) = sb[i];
+        }
+    };
+    bf16x8 fa_[4], fb_[4], ga_[4], gb_[4];  // fragments of the current / next k-step
+    auto read = [&](const char* st, int ks, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = frag_tr(st, 16 * ks, 128 * wm + 32 * i, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = frag_tr(st + IMG, 16 * ks, 128 * wn + 32 * j, lane);
+    };
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto mfmas = [&](const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fa::mfma(b[j], a[i], acc[i][j]);
+    };
+
+    // prologue: tile 0 in LDS buffer 0, tile 1 in flight in the staging registers, k-step 0 fragments read
+    load(0);
+    store(smem);
+    if (nk > 1) load(1);
+    __syncthreads();
+    read(smem, 0, fa_, fb_);
+    for (int t = 0; t < nk; ++t) {
+        const char* cur = smem + (t & 1) * STAGE;
+        char* nxt = smem + ((t + 1) & 1) * STAGE;
+        read(cur, 1, ga_, gb_);
+        mfmas(fa_, fb_);  // k-step 0
+        __builtin_amdgcn_sched_barrier(0);
+        read(cur, 2, fa_, fb_);
+        mfmas(ga_, gb_);  // k-step 1
+        __builtin_amdgcn_sched_barrier(0);
+        read(cur, 3, ga_, gb_);
+        if (t + 1 < nk) store(nxt);  // tile t+1 (staged during tile t-1) -> the buffer tile t-1 used
+        if (t + 2 < nk) load(t + 2);
+        mfmas(fa_, fb_);  // k-step 2
+        __builtin_amdgcn_sched_barrier(0);
+        // tile t+1's image complete and every wave done reading tile t's k-steps (k-step 3 is in registers)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) read(nxt, 0, fa_, fb_);
+        mfmas(ga_, gb_);  // k-step 3
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    const int h = lane >> 5, c = lane & 31;
+    if (unit >= 0) {  // K-slice of a tail tile: fp32 partial [256][256] at ws + unit * 65536
+        float* wp = ws + (int64_t)unit * 65536;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float* rp = wp + (128 * wm + 32 * i + c) * 256 + 128 * wn + 4 * h;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f32x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(rp + 32 * j + 8 * q) = o;
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 32 * i + c) * ldc + n0 + 128 * wn + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            u16x4 old[4];
+            if (BETA) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) old[q] = *reinterpret_cast<const u16x4*>(crow_p + 32 * j + 8 * q);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = acc[i][j][4 * q + e];
+                    if (BETA) x += bf2f(old[q][e]);
+                    o[e] = f2bf(x);
+                }
+                *reinterpret_cast<u16x4*>(crow_p + 32 * j + 8 * q) = o;
+            }
+        }
+    }
+}
+template __global__ void gemm_tn_w4_kernel<true>(const u16* __restrict__, int, const u16* __restrict__, int,
+                                                 u16* __restrict__, int, int, int, int, int, int, float* __restrict__);
+template __global__ void gemm_tn_w4_kernel<false>(const u16* __restrict__, int, const u16* __restrict__, int,
+                                                  u16* __restrict__, int, int, int, int, int, int, float* __restrict__);
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -837,6 +996,20 @@ void launch_tn_il(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
                            (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
 }
 
+template <bool BETA>
+void launch_tn_w4(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+                  int64_t K, hipStream_t st, int full_blocks, int split, float* ws) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
+    const int grid = full_blocks + (nwg - full_blocks) * split;
+    hipLaunchKernelGGL((gemm_tn_w4_kernel<BETA>), dim3(grid), dim3(256), 2 * Cfg<64>::kStage, st, (const u16*)A,
+                       (int)lda, (const u16*)B, (int)ldb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, full_blocks, split,
+                       ws);
+    if (split > 1)
+        hipLaunchKernelGGL(gemm_tn_combine_kernel, dim3(nwg - full_blocks, 64), dim3(256), 0, st, (const float*)ws, (u16*)C,
+                           (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
+}
+
 template <bool BETA, int BK, int STAGES, bool LW>
 void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                int64_t K, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr) {
@@ -860,7 +1033,8 @@ namespace sa_launch {
 // pipeline variants (benchmarking hook): 2 (default) = BK 64 x 2 stages, split staging (one 32-MFMA block per
 // phase); 5 = the same with three B buffers (B staged in group 1's read window); 0 = BK 32 x 4 stages, wait behind
 // the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2;
-// 6 = no ping-pong, reads interleaved with each wave's own MFMAs (gemm_tn_il_kernel)
+// 6 = no ping-pong, reads interleaved with each wave's own MFMAs (gemm_tn_il_kernel); 7 = one wave per SIMD,
+// 128x128 wave tiles, register-staged (gemm_tn_w4_kernel)
 static int g_gemm_variant = 2;
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 // profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
@@ -896,7 +1070,8 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     const int nwg = (int)((M / 256) * (N / 256));
     full_blocks = nwg;
     split = 1;
-    if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6) || slots <= 0) return 0;
+    if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6 && g_gemm_variant != 7) || slots <= 0)
+        return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
     if (r == 0) return 0;
     // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
@@ -917,6 +1092,11 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
     if (g_gemm_variant == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        return;
+    }
+    if (g_gemm_variant == 7) {
+        if (beta) launch_tn_w4<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        else launch_tn_w4<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
     if (g_gemm_variant == 6) {

@@ -25,6 +25,9 @@ void swiglu_bwd(int dtype, const void* dy, const void* a, const void* b, int64_t
 void rope(int dtype, bool interleaved, const void* x, int64_t x_tok, int64_t x_head, void* out, int64_t o_tok,
           int64_t o_head, const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd,
           int seq_len, float sign, hipStream_t st);
+// graph decode: RoPE(q) -> q_out, RoPE(k) -> K cache row *pos, v -> V cache row *pos (one token); false = unsupported
+bool rope_kv_append(int dtype, bool interleaved, const void* x, void* q_out, void* kc, void* vc, const int64_t* pos,
+                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, hipStream_t st);
 }  // namespace sa_launch
 
 namespace sa_launch {

@@ -155,12 +155,94 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
     }
 }
 
+// Graph-decode step (one token): RoPE of the q and k heads and the K/V cache append in ONE launch.  x is the QKV
+// projection row [nq + 2 nkv heads][hd] (contiguous); q heads are rotated into q_out [nq][hd]; k heads are rotated
+// straight into row *pos of the K cache and v heads copied into row *pos of the V cache ([cap][nkv][hd] each) --
+// replacing rope(q), rope(k) and two index_copy launches.  One work item = 8 pair slots (as rope_v8_kernel).
+template <typename T, bool IL>
+__global__ __launch_bounds__(256) void rope_kv_append_kernel(const T* __restrict__ x, T* __restrict__ q_out,
+                                                             T* __restrict__ kc, T* __restrict__ vc,
+                                                             const int64_t* __restrict__ pos, const float* cosb,
+                                                             const float* sinb, int nq, int nkv, int hd, int rd) {
+    const int half = rd / 2;
+    const int rc = IL ? rd / 8 : half / 8;
+    const int CR = rc + (hd - rd) / 8;
+    const int nh = nq + 2 * nkv;
+    const int64_t ps = pos[0];
+    const int n = nh * CR;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int h = i / CR, c = i - h * CR;
+        const T* xr = x + (int64_t)h * hd;
+        T* orow;
+        if (h < nq) orow = q_out + (int64_t)h * hd;
+        else if (h < nq + nkv) orow = kc + (ps * nkv + (h - nq)) * hd;
+        else orow = vc + (ps * nkv + (h - nq - nkv)) * hd;
+        if (h >= nq + nkv) {  // v: plain copy of the row's chunks
+            for (int e = 8 * c; e < hd; e += 8 * CR) {
+                float v[8];
+                V8<T>::ld(xr + e, v);
+                V8<T>::st(orow + e, v);
+            }
+            continue;
+        }
+        if (c < rc) {
+            const float* cb = cosb + ps * half;
+            const float* sb = sinb + ps * half;
+            if (!IL) {
+                const int p = c * 8;
+                float x0[8], x1[8], cs[8], sn[8], o0[8], o1[8];
+                V8<T>::ld(xr + p, x0);
+                V8<T>::ld(xr + half + p, x1);
+                V8<float>::ld(cb + p, cs);
+                V8<float>::ld(sb + p, sn);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    o0[j] = x0[j] * cs[j] - x1[j] * sn[j];
+                    o1[j] = x1[j] * cs[j] + x0[j] * sn[j];
+                }
+                V8<T>::st(orow + p, o0);
+                V8<T>::st(orow + half + p, o1);
+            } else {
+                const int e = c * 8;
+                float v[8], o[8];
+                V8<T>::ld(xr + e, v);
+                const f32x4 cs = *reinterpret_cast<const f32x4*>(cb + e / 2);
+                const f32x4 sn = *reinterpret_cast<const f32x4*>(sb + e / 2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[2 * j] = v[2 * j] * cs[j] - v[2 * j + 1] * sn[j];
+                    o[2 * j + 1] = v[2 * j + 1] * cs[j] + v[2 * j] * sn[j];
+                }
+                V8<T>::st(orow + e, o);
+            }
+        } else {
+            const int e = rd + (c - rc) * 8;
+            float v[8];
+            V8<T>::ld(xr + e, v);
+            V8<T>::st(orow + e, v);
+        }
+    }
+}
+
 static int grid_for(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
 }
 
 namespace sa_launch {
+bool rope_kv_append(int dtype, bool interleaved, const void* x, void* q_out, void* kc, void* vc, const int64_t* pos,
+                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, hipStream_t st) {
+    if (dtype == DT_F32 || hd % 8 || (interleaved ? rd % 8 : rd % 16)) return false;
+    const int CR = (interleaved ? rd / 8 : rd / 16) + (hd - rd) / 8;
+    const int g = grid_for((int64_t)(nq + 2 * nkv) * CR);
+#define SA_RKV(TT, IL)                                                                                            \
+    hipLaunchKernelGGL((rope_kv_append_kernel<TT, IL>), g, 256, 0, st, (const TT*)x, (TT*)q_out, (TT*)kc, (TT*)vc, \
+                       pos, cosb, sinb, nq, nkv, hd, rd)
+    if (dtype == DT_BF16) { if (interleaved) SA_RKV(u16, true); else SA_RKV(u16, false); }
+    else { if (interleaved) SA_RKV(f16, true); else SA_RKV(f16, false); }
+#undef SA_RKV
+    return true;
+}
 void swiglu_fwd(int dtype, const void* a, const void* b, int64_t lda, void* out, int64_t rows, int F, hipStream_t st) {
     const int g = grid_for(rows * (F / 8));
     if (dtype == DT_BF16) hipLaunchKernelGGL(swiglu_fwd_kernel<u16>, g, 256, 0, st, (const u16*)a, (const u16*)b, lda, (u16*)out, rows, F);

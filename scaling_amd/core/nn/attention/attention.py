@@ -21,6 +21,7 @@ from typing import Any, Callable, Optional, Union
 import torch
 
 from ....ops import attention as attn_ops
+from ....ops._ext import ext, use_native
 from ...topology import Topology
 from ..linear import ColumnParallelLinear, RowParallelLinear
 from ..linear.fused import fused_column_linear
@@ -455,6 +456,30 @@ class ParallelSelfAttention(torch.nn.Module):
                 value = value + out
         return [query, key, value]
 
+    def _decode_rope_append(self, base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                            position_ids: Optional[torch.Tensor], cache_index: int) -> Optional[tuple]:
+        """One-token step of graph-captured decoding: rotate q and k and append k/v at the cache's device-side
+        position with ONE kernel (``ext().rope_kv_append``) instead of two RoPE launches and two ``index_copy_``.
+        Applies when q/k/v are the [q | k | v] column blocks of one projection row and the token's position ids ARE
+        the cache position tensor; None otherwise (the caller runs the unfused ops)."""
+        kv = self.cache.get(cache_index)
+        re = self.rotary_embedding
+        if not (isinstance(kv, StaticKVCache) and re is not None and self.use_flash_attention and use_native(base)):
+            return None
+        if position_ids is None or position_ids.numel() != 1 or position_ids.data_ptr() != kv.state.pos.data_ptr():
+            return None
+        hd, nq, nkv = self.hidden_size_per_attention_head, q.shape[1], k.shape[1]
+        es = base.element_size()
+        if not (base.is_contiguous() and base.numel() == (nq + 2 * nkv) * hd and q.data_ptr() == base.data_ptr()
+                and k.data_ptr() == base.data_ptr() + nq * hd * es and v.data_ptr() == base.data_ptr() + (nq + nkv) * hd * es
+                and q.stride(1) == hd and k.stride(1) == hd and v.stride(1) == hd):
+            return None
+        qr = ext().rope_kv_append(base, re.cos_table, re.sin_table, kv.state.pos, nq, nkv, re.dimensions, re.interleaved,
+                                  kv.k, kv.v)
+        if qr is None:
+            return None
+        return qr, kv.k, kv.v, kv.state.cu_k
+
     # ------------------------------------------------------------------ forward
     def forward(
         self,
@@ -488,12 +513,17 @@ class ParallelSelfAttention(torch.nn.Module):
             assert self.norm_query is not None and self.norm_key is not None
             q = all_shard(self.norm_query(all_concat(q, dim=1, topology=self.topology)), dim=1, topology=self.topology)
             k = all_shard(self.norm_key(all_concat(k, dim=1, topology=self.topology)), dim=1, topology=self.topology)
-        if self.rotary_embedding is not None:
+        fused_append = None
+        if use_cache and not reset_cache and T == 1 and not self.key_query_norm:
+            fused_append = self._decode_rope_append(base, q, k, v, position_ids, cache_index)
+        if fused_append is not None:  # graph decode: RoPE + K/V cache append in one launch
+            q, k, v, cumulative_seq_lengths_key = fused_append
+        elif self.rotary_embedding is not None:
             pos = position_ids.reshape(-1) if position_ids is not None else None
             q = self.rotary_embedding.apply_tokens(q, pos, s)
             k = self.rotary_embedding.apply_tokens(k, pos, s)
 
-        if use_cache:
+        if use_cache and fused_append is None:
             if not self.causal:
                 raise ValueError("KV caching is only supported for causal attention.")
             assert b == 1, f"KV caching is only supported for batch size 1, got {b}"

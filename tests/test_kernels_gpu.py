@@ -485,12 +485,13 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 4, 5, 6])
+@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
 def test_gemm_tn(M, N, K, accumulate, variant):
     """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands; pipeline
-    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers) and 6 (no ping-pong)."""
+    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers), 6 (no ping-pong) and 7 (one wave per
+    SIMD, register-staged)."""
     ext().gemm_set_variant(variant)
     try:
         _gemm_tn_case(M, N, K, accumulate)
@@ -779,3 +780,29 @@ def test_gemv_epilogues_bit_identical(rows, dtype):
     # against fp32 math
     hf = torch.nn.functional.silu(x.float() @ w[:F].float().t()) * (x.float() @ w[F:].float().t())
     torch.testing.assert_close(h.float(), hf, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("interleaved", [False, True])
+@pytest.mark.parametrize("rot_frac", [1.0, 0.5])
+def test_rope_kv_append_bit_identical(interleaved, rot_frac):
+    """Graph-decode step kernel: RoPE(q), RoPE(k) into the K cache row at the device position, v into the V cache
+    row -- one launch, bit-identical to rope() twice + two index_copy_."""
+    torch.manual_seed(3)
+    nq, nkv, hd, cap = 8, 2, 128, 64
+    rd = int(hd * rot_frac)
+    half = rd // 2
+    inv = 1.0 / (10000 ** (torch.arange(0, half, device=DEV, dtype=torch.float32) / half))
+    ang = torch.arange(cap, device=DEV, dtype=torch.float32)[:, None] * inv[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    qkv = torch.randn(1, nq + 2 * nkv, hd, device=DEV, dtype=torch.bfloat16)
+    pos = torch.tensor([37], device=DEV, dtype=torch.long)
+    kc = torch.randn(cap, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(cap, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    q_ref = ext().rope(qkv[:, :nq], cos, sin, pos, rd, 1, interleaved, False)
+    k_ref = ext().rope(qkv[:, nq:nq + nkv], cos, sin, pos, rd, 1, interleaved, False)
+    kc_ref.index_copy_(0, pos, k_ref)
+    vc_ref.index_copy_(0, pos, qkv[:, nq + nkv:])
+    q = ext().rope_kv_append(qkv, cos, sin, pos, nq, nkv, rd, interleaved, kc, vc)
+    assert q is not None
+    assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
