@@ -872,19 +872,34 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const u16* __restric
     if (nk > 1) load(1);
     __syncthreads();
     read(smem, 0, fa_, fb_);
+    // issue order inside a k-step: one fragment read (and in k-step 2 one ds_write + one global load) per MFMA gap
+    auto interleave = [&](int extra) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            if (extra) {
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            }
+        }
+    };
     for (int t = 0; t < nk; ++t) {
         const char* cur = smem + (t & 1) * STAGE;
         char* nxt = smem + ((t + 1) & 1) * STAGE;
         read(cur, 1, ga_, gb_);
         mfmas(fa_, fb_);  // k-step 0
+        interleave(0);
         __builtin_amdgcn_sched_barrier(0);
         read(cur, 2, fa_, fb_);
         mfmas(ga_, gb_);  // k-step 1
+        interleave(0);
         __builtin_amdgcn_sched_barrier(0);
         read(cur, 3, ga_, gb_);
         if (t + 1 < nk) store(nxt);  // tile t+1 (staged during tile t-1) -> the buffer tile t-1 used
         if (t + 2 < nk) load(t + 2);
         mfmas(fa_, fb_);  // k-step 2
+        interleave(1);
         __builtin_amdgcn_sched_barrier(0);
         // tile t+1's image complete and every wave done reading tile t's k-steps (k-step 3 is in registers)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -892,6 +907,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const u16* __restric
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < nk) read(nxt, 0, fa_, fb_);
         mfmas(ga_, gb_);  // k-step 3
+        interleave(0);
         __builtin_amdgcn_sched_barrier(0);
     }
 
