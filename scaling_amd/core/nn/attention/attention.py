@@ -15,6 +15,7 @@ MI355X-first:
 from __future__ import annotations
 
 import math
+import os
 from enum import Enum
 from typing import Any, Callable, Optional, Union
 
@@ -48,6 +49,9 @@ def repeat_kv(x: torch.Tensor, n_rep: int) -> torch.Tensor:
     if n_rep == 1:
         return x
     return x.repeat_interleave(n_rep, dim=-2)
+
+# graph-decode step kernels (RoPE + K/V cache append in one launch); SCALING_AMD_DECODE_FUSED=0 for A/B
+_DECODE_FUSED = os.environ.get("SCALING_AMD_DECODE_FUSED", "1") != "0"
 
 
 def get_max_seq_length(cumulative_seq_lengths: torch.Tensor) -> int:
@@ -514,7 +518,7 @@ class ParallelSelfAttention(torch.nn.Module):
             q = all_shard(self.norm_query(all_concat(q, dim=1, topology=self.topology)), dim=1, topology=self.topology)
             k = all_shard(self.norm_key(all_concat(k, dim=1, topology=self.topology)), dim=1, topology=self.topology)
         fused_append = None
-        if use_cache and not reset_cache and T == 1 and not self.key_query_norm:
+        if use_cache and not reset_cache and T == 1 and not self.key_query_norm and _DECODE_FUSED:
             fused_append = self._decode_rope_append(base, q, k, v, position_ids, cache_index)
         if fused_append is not None:  # graph decode: RoPE + K/V cache append in one launch
             q, k, v, cumulative_seq_lengths_key = fused_append
