@@ -267,3 +267,40 @@ def test_async_checkpoint_snapshot_handles_dict_subclasses_and_mutable_leaves():
     assert snap["s"] == {1, 2}
     assert torch.equal(snap["d"]["a"][0], torch.ones(2))
     assert type(snap["nt"]).__name__ == "NT" and snap["nt"].y == 3
+
+
+@pytest.mark.parametrize("pp", [1, 2, 7, 16, 32])
+def test_schedule_visualize_grid_and_inference_independent_of_acc(tmp_path, pp):
+    """Reference tests/core/test_nn/test_pipeline_schedule.py grid: the train schedule renders for every (pp, acc);
+    the inference schedule renders for acc 1 and 2 (acc + pp - 1 steps, so more micro-batches draw wider)."""
+    from scaling_amd.core import PipelineScheduleInference, PipelineScheduleTrain
+
+    for acc in (1, 2, 7, 16, 32):
+        PipelineScheduleTrain.visualize(gradient_accumulation_steps=acc, pipe_parallel_size=pp)
+    a = PipelineScheduleInference.visualize(gradient_accumulation_steps=1, pipe_parallel_size=pp)
+    b = PipelineScheduleInference.visualize(gradient_accumulation_steps=2, pipe_parallel_size=pp)
+    assert a.size[1] == b.size[1] and b.size[0] > a.size[0]
+
+
+def test_visualize_measured_profile(tmp_path):
+    """A profile written by the framework's own profiler (2-stage pipeline training run) replays through the
+    schedule simulator (reference test_visualize_train_profile): per-stage busy / idle times and an image."""
+    import json
+
+    from scaling_amd.core import PipelineScheduleTrain
+    from tests.test_training import _config, _make_data, _run
+
+    _make_data(tmp_path / "data")
+    cfg = _config(tmp_path, 1, 2, 2)
+    cfg["trainer"]["save_dir"] = None
+    cfg["trainer"]["load_dir"] = None
+    cfg["trainer"]["train_iterations"] = 3
+    _run(tmp_path, cfg, 2, "prof")
+    prof = next((tmp_path / "logs").rglob("profile.json"))
+    d = json.loads(prof.read_text())
+    assert d["pipe_parallel_size"] == 2 and d["observations"]
+    timings, image = PipelineScheduleTrain.visualize_profile(profile_file=prof, milliseconds_per_pixel=0.01,
+                                                             pipe_pixels=50)
+    assert timings["total_time"] > 0
+    assert all(0.0 <= v < 1.0 for v in timings["pct_idling"].values())
+    image.save(str(tmp_path / "profile.png"))
