@@ -958,6 +958,202 @@ template __global__ void gemm_tn_w4_kernel<true>(const u16* __restrict__, int, c
 template __global__ void gemm_tn_w4_kernel<false>(const u16* __restrict__, int, const u16* __restrict__, int,
                                                   u16* __restrict__, int, int, int, int, int, int, float* __restrict__);
 
+// ---------------------------------------------------------------------------------------------------------------
+// Variant 8: one wave per SIMD on v_mfma_f32_16x16x32_bf16, both operands by LDS-DMA.  The shape of the vendor
+// library's fastest forward kernel on this chip (256x256x64 macro tile, 4 waves x 128x128, 16x16x32 MFMAs, DMA pieces
+// threaded between the MFMAs, one barrier per K-tile), with the operand fragments produced by transposing LDS reads
+// because both wgrad operands are k-strided.
+//  * 64 MFMAs of 16 cycles per 32-deep k-step per wave (8 x 8 tiles of 16x16, 256 fp32 accumulators per lane in the
+//    unified register file); 16 fragments per k-step = 32 ds_read_b64_tr_b16 (0.5 per MFMA);
+//  * per 64-deep K-tile each wave stages 8 one-KiB pieces of the A image and 8 of the B image (koff16 swizzle, the
+//    images of variant 4);
+//  * fragment addresses are per-lane offsets precomputed for both stages (the loop is unrolled by two tiles so the
+//    stage is a constant); k-step, second read and image offsets ride in the ds_read immediate.
+// in-place accumulate in AGPRs: with 256 live fp32 accumulators per lane the register allocator otherwise
+// rotates them through copies (v_accvgpr_read/write/mov per MFMA) and spills the fragments
+__device__ __forceinline__ void mfma16_acc(f32x4& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+
+template <bool BETA>
+__global__ __launch_bounds__(256, 1) void gemm_tn_w4m16_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                               const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                               u16* __restrict__ C, int ldc, int M, int N, int K,
+                                                               int full_blocks, int tail_split, float* __restrict__ ws) {
+    constexpr int BK = 64;
+    using G = Cfg<BK>;
+    constexpr int NW = 4;                         // every wave stages both images
+    constexpr int NP = G::kImg / 1024 / NW;       // 8 pieces per wave per image
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    const int tm = M / 256, tn = N / 256;
+    int v, k_lo = 0, nk = K / BK, unit = -1;
+    if ((int)blockIdx.x < full_blocks) {
+        v = xcd_remap(blockIdx.x, full_blocks);
+    } else {
+        unit = (int)blockIdx.x - full_blocks;
+        v = full_blocks + unit / tail_split;
+        nk /= tail_split;
+        k_lo = (unit % tail_split) * nk;
+    }
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    Dma16<NP, NW> da, db;
+    da.init(wave, lane, lda);
+    db.init(wave, lane, ldb);
+    auto soff_a = [&](int t) { return __builtin_amdgcn_readfirstlane(((k_lo + t) * BK * lda + m0) * 2); };
+    auto soff_b = [&](int t) { return __builtin_amdgcn_readfirstlane(((k_lo + t) * BK * ldb + n0) * 2); };
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // per-lane LDS byte offsets of the 16 fragments (k-step 0, first transposing read) in each stage
+    int oa[2][8], ob[2][8];
+    {
+        const int g = lane >> 4, i16 = lane & 15;
+        const int row = 4 * g + (i16 >> 2), cl = 4 * (i16 & 3);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                oa[s][i] = s * G::kStage + koff16(row, 128 * wm + 16 * i + cl);
+                ob[s][i] = s * G::kStage + G::kImg + koff16(row, 128 * wn + 16 * i + cl);
+            }
+    }
+    auto frag = [&](int off, int ks) -> bf16x8 {
+        const char* p = smem + off + ks * 32 * 512;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 16 * 512));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+#define SA_W16_READ(S, KS, FA, FB)                                                \
+    {                                                                             \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) FB[j] = frag(ob[S][j], KS); \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) FA[i] = frag(oa[S][i], KS); \
+    }
+    // One 64-deep K-tile t in LDS stage S (tile t+1 in flight into stage 1-S).  k-step 0 multiplies beside the
+    // k-step 1 fragment reads (one per two MFMAs); one barrier (every read of stage S retired, this wave's pieces of
+    // tile t+1 landed); k-step 1 multiplies beside tile t+1's k-step 0 reads (first half, one per MFMA) and tile t+2's
+    // pieces into stage S (second half, one per two MFMAs).  Branch-free: after the last tile the reads hit the other
+    // stage harmlessly and the last two tiles re-stage tile nk-1 into a stage never read again.
+#define SA_W16_TILE(S, T)                                                                                       \
+    {                                                                                                           \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
+                mfma16_acc(acc[i][j], fb0[j], fa0[i]);                                                          \
+                const int m_ = i * 8 + j;                                                                       \
+                if ((m_ & 3) == 3) {                                                                            \
+                    const int f_ = m_ >> 2;                                                                     \
+                    if (f_ < 8) fb1[f_] = frag(ob[S][f_], 1);                                                   \
+                    else fa1[f_ - 8] = frag(oa[S][f_ - 8], 1);                                                  \
+                }                                                                                               \
+            }                                                                                                   \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
+        wait_vm<0>();                                                                                           \
+        hard_barrier();                                                                                         \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
+                mfma16_acc(acc[i][j], fb1[j], fa1[i]);                                                          \
+                const int m_ = i * 8 + j;                                                                       \
+                if ((m_ & 1) == 1) {                                                                            \
+                    const int f_ = m_ >> 1;                                                                     \
+                    if (f_ < 8) fb0[f_] = frag(ob[1 - (S)][f_], 0);                                             \
+                    else fa0[f_ - 8] = frag(oa[1 - (S)][f_ - 8], 0);                                            \
+                }                                                                                               \
+            }                                                                                                   \
+        {                                                                                                       \
+            const int t2_ = min((T) + 2, nk - 1);                                                               \
+            const int sa_ = soff_a(t2_), sb_ = soff_b(t2_);                                                     \
+            char* st_ = smem + (S) * G::kStage;                                                                 \
+            _Pragma("unroll") for (int i = 4; i < 8; ++i)                                                       \
+                _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                 \
+                    mfma16_acc(acc[i][j], fb1[j], fa1[i]);                                                      \
+                    const int m_ = (i - 4) * 8 + j;                                                             \
+                    if ((m_ & 1) == 1) {                                                                        \
+                        const int p_ = m_ >> 1;                                                                 \
+                        if ((p_ & 1) == 0) da.load_piece_nc(p_ >> 1, A, a_bytes, sa_, st_, wave);               \
+                        else db.load_piece_nc(p_ >> 1, B, b_bytes, sb_, st_ + G::kImg, wave);                   \
+                    }                                                                                           \
+                }                                                                                               \
+        }                                                                                                       \
+    }
+
+    // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, its k-step 0 fragments read
+    da.load(A, a_bytes, soff_a(0), smem, wave);
+    db.load(B, b_bytes, soff_b(0), smem + G::kImg, wave);
+    if (nk > 1) {
+        da.load(A, a_bytes, soff_a(1), smem + G::kStage, wave);
+        db.load(B, b_bytes, soff_b(1), smem + G::kStage + G::kImg, wave);
+        wait_vm<2 * NP>();
+    } else {
+        wait_vm<0>();
+    }
+    hard_barrier();
+    SA_W16_READ(0, 0, fa0, fb0)
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+        SA_W16_TILE(0, t)
+        SA_W16_TILE(1, t + 1)
+    }
+    if (t < nk) SA_W16_TILE(0, t)
+#undef SA_W16_TILE
+#undef SA_W16_READ
+    wait_vm<0>();
+    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    // epilogue: acc[i][j][e] = C[m0 + 128wm + 16i + (lane & 15)][n0 + 128wn + 16j + 4(lane >> 4) + e]
+    const int r = lane & 15, q4 = 4 * (lane >> 4);
+    if (unit >= 0) {  // K-slice of a tail tile: fp32 partial [256][256] at ws + unit * 65536
+        float* wp = ws + (int64_t)unit * 65536;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float* rp = wp + (128 * wm + 16 * i + r) * 256 + 128 * wn + q4;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4*>(rp + 16 * j) = acc[i][j];
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ldc + n0 + 128 * wn + q4;
+        u16x4 old[8];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = acc[i][j][e];
+                if (BETA) x += bf2f(old[j][e]);
+                o[e] = f2bf(x);
+            }
+            *reinterpret_cast<u16x4*>(crow_p + 16 * j) = o;
+        }
+    }
+}
+template __global__ void gemm_tn_w4m16_kernel<true>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                    int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
+                                                    float* __restrict__);
+template __global__ void gemm_tn_w4m16_kernel<false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                     int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
+                                                     float* __restrict__);
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -1026,6 +1222,21 @@ void launch_tn_w4(const void* A, int64_t lda, const void* B, int64_t ldb, void* 
                            (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
 }
 
+template <bool BETA>
+void launch_tn_w4m16(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
+                     int64_t N, int64_t K, hipStream_t st, int full_blocks, int split, float* ws) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
+    const int grid = full_blocks + (nwg - full_blocks) * split;
+    const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+    hipLaunchKernelGGL((gemm_tn_w4m16_kernel<BETA>), dim3(grid), dim3(256), 2 * Cfg<64>::kStage, st, (const u16*)A,
+                       (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, full_blocks,
+                       split, ws);
+    if (split > 1)
+        hipLaunchKernelGGL(gemm_tn_combine_kernel, dim3(nwg - full_blocks, 64), dim3(256), 0, st, (const float*)ws, (u16*)C,
+                           (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
+}
+
 template <bool BETA, int BK, int STAGES, bool LW>
 void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                int64_t K, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr) {
@@ -1086,7 +1297,9 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     const int nwg = (int)((M / 256) * (N / 256));
     full_blocks = nwg;
     split = 1;
-    if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6 && g_gemm_variant != 7) || slots <= 0)
+    if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6 && g_gemm_variant != 7 &&
+         g_gemm_variant != 8) ||
+        slots <= 0)
         return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
     if (r == 0) return 0;
@@ -1108,6 +1321,11 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
     if (g_gemm_variant == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        return;
+    }
+    if (g_gemm_variant == 8) {
+        if (beta) launch_tn_w4m16<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        else launch_tn_w4m16<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
     if (g_gemm_variant == 7) {
