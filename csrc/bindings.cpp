@@ -620,6 +620,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
     m.def("gemm_set_variant", &sa_launch::gemm_set_variant, "select the gemm_tn pipeline variant (benchmarking)");
+    m.def("gemm_get_variant", &sa_launch::gemm_get_variant, "the current gemm_tn pipeline variant");
     m.def("gemm_tn_timing", &gemm_tn_timing, "profiling: per-phase s_memtime stamps of gemm_tn workgroup 0");
     m.def("ar_alloc", &ar_alloc, "one-shot all-reduce: allocate + IPC-export a registered buffer");
     m.def("ar_open", &ar_open, "one-shot all-reduce: map a peer's registered buffer");

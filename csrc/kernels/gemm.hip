@@ -1154,6 +1154,242 @@ template __global__ void gemm_tn_w4m16_kernel<false>(const u16* __restrict__, in
                                                      int, uint32_t, u16* __restrict__, int, int, int, int, int, int,
                                                      float* __restrict__);
 
+// ---------------------------------------------------------------------------------------------------------------
+// Variant 9: variant 8's wave layout (4 waves x 128x128, 16x16x32 MFMAs, in-place AGPR accumulators) on a four-slot
+// LDS ring of 32-deep k-steps (A and B images [32][256] bf16 per slot, 4 x 32 KiB) instead of two 64-deep stages:
+//  * during k-step t each wave multiplies F_t (in registers), reads F_{t+1} from slot (t+1)%4 (16 fragments over the
+//    first 48 MFMAs) and stages k-step t+4 into slot t%4 (8 one-KiB pieces, one per 8 MFMAs);
+//  * one barrier per k-step: every wave's reads of slot (t+1)%4 retired and k-step t+2 landed (vmcnt leaves the
+//    16 pieces of k-steps t+3 and t+4 in flight), so each piece has 2-3 k-steps (2-3k cycles) to land instead of 1-2.
+//  SCHED: 0 = F_{t+1} reads one per 3 MFMAs over the first 48, pieces one per 8 MFMAs; 1 = reads one per 2 MFMAs over
+//  the first 32, pieces one per 4 over the last 32; 2 = reads one per 4 MFMAs, pieces one per 8 (offset by 4).
+//  FASTDMA: 0 = Dma::load_piece_nc (descriptor rebuilt per piece, m0 saved / restored); 1 = descriptors built once,
+//  m0 clobbered (the compiler emits no other m0 use in this kernel, but an m0 clobber is only a warning to it);
+//  2 = descriptors built once, m0 saved / restored around each piece.
+//  SCHED 3 = SCHED 1 with the pieces one per 2 MFMAs over MFMAs 32-47 (they land earlier).
+//  TIMING: s_memtime stamps of workgroup 0, k-steps 32-39, events 0 top, 1 MFMA stream issued, 2 reads retired,
+//  3 pieces landed, 4 past the barrier (LDS past the ring, then dbg[wave][step][event]).
+template <bool BETA, int SCHED = 0, int FASTDMA = 0, bool TIMING = false>
+__global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                              const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                              u16* __restrict__ C, int ldc, int M, int N, int K,
+                                                              int full_blocks, int tail_split, float* __restrict__ ws,
+                                                              uint64_t* __restrict__ dbg = nullptr) {
+    constexpr int BK = 32;
+    using G = Cfg<BK>;                            // kImg 16 KiB, kStage 32 KiB
+    constexpr int NW = 4;
+    constexpr int NP = G::kImg / 1024 / NW;       // 4 pieces per wave per image
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+
+    const int tm = M / 256, tn = N / 256;
+    int v, k_lo = 0, nk = K / 64, unit = -1;      // 64-deep tiles (the split plan's unit)
+    if ((int)blockIdx.x < full_blocks) {
+        v = xcd_remap(blockIdx.x, full_blocks);
+    } else {
+        unit = (int)blockIdx.x - full_blocks;
+        v = full_blocks + unit / tail_split;
+        nk /= tail_split;
+        k_lo = (unit % tail_split) * nk;
+    }
+    const int ns = 2 * nk, s_lo = 2 * k_lo;      // 32-deep k-steps of this block
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+
+    Dma16<NP, NW> da, db;
+    da.init(wave, lane, lda);
+    db.init(wave, lane, ldb);
+    auto soff_a = [&](int u) { return __builtin_amdgcn_readfirstlane(((s_lo + min(u, ns - 1)) * BK * lda + m0) * 2); };
+    auto soff_b = [&](int u) { return __builtin_amdgcn_readfirstlane(((s_lo + min(u, ns - 1)) * BK * ldb + n0) * 2); };
+    auto stage_all = [&](int u, int slot) {
+        da.load(A, a_bytes, soff_a(u), smem + slot * G::kStage, wave);
+        db.load(B, b_bytes, soff_b(u), smem + slot * G::kStage + G::kImg, wave);
+    };
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // per-lane fragment offsets for slot pairs {0,1} and {2,3}; slot parity (32 KiB), B image (16 KiB) and the second
+    // transposing read (+16 rows = 8 KiB) ride in the ds_read immediate (< 64 KiB)
+    int oa[2][8], ob[2][8];
+    {
+        const int g = lane >> 4, i16 = lane & 15;
+        const int row = 4 * g + (i16 >> 2), cl = 4 * (i16 & 3);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                oa[h][i] = h * 2 * G::kStage + koff16(row, 128 * wm + 16 * i + cl);
+                ob[h][i] = h * 2 * G::kStage + G::kImg + koff16(row, 128 * wn + 16 * i + cl);
+            }
+    }
+    auto frag = [&](int off, int slot) -> bf16x8 {
+        const char* p = smem + off + (slot & 1) * G::kStage;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p + 16 * 512));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+#define SA_RING_READ(SLOT, FA, FB, F)                                         \
+    {                                                                         \
+        if ((F) < 8) FB[(F)] = frag(ob[(SLOT) >> 1][(F)], (SLOT));            \
+        else FA[(F) - 8] = frag(oa[(SLOT) >> 1][(F) - 8], (SLOT));            \
+    }
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 rsa = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(A)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(A) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(a_bytes), fa::kBufFlags};
+    const i32x4 rsb = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(B)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(B) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(b_bytes), fa::kBufFlags};
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)smem));
+    // piece P (0..7: even = A piece P/2, odd = B piece P/2) of k-step U into slot SLOT
+#define SA_RING_PIECE(P, SLOT, SA, SB, ST)                                                                       \
+    {                                                                                                            \
+        if constexpr (FASTDMA != 0) {                                                                            \
+            const bool isb_ = ((P) & 1) != 0;                                                                    \
+            const int i_ = (P) >> 1;                                                                             \
+            const uint32_t l_ = lds0 + (SLOT) * G::kStage + (isb_ ? G::kImg : 0) + (wave + NW * i_) * 1024;    \
+            if constexpr (FASTDMA == 1) {                                                                        \
+                if (isb_)                                                                                        \
+                    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"      \
+                                 ::"s"(l_), "v"(db.voff), "s"(rsb), "s"((SB) + i_ * db.step) : "m0");           \
+                else                                                                                             \
+                    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"      \
+                                 ::"s"(l_), "v"(da.voff), "s"(rsa), "s"((SA) + i_ * da.step) : "m0");           \
+            } else {                                                                                             \
+                int keep_;                                                                                       \
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"                              \
+                             "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"                     \
+                             : "=&s"(keep_)                                                                      \
+                             : "s"(l_), "v"(isb_ ? db.voff : da.voff), "s"(isb_ ? rsb : rsa),                   \
+                               "s"(isb_ ? (SB) + i_ * db.step : (SA) + i_ * da.step));                          \
+            }                                                                                                    \
+        } else {                                                                                                 \
+            if (((P) & 1) == 0) da.load_piece_nc((P) >> 1, A, a_bytes, (SA), (ST), wave);                      \
+            else db.load_piece_nc((P) >> 1, B, b_bytes, (SB), (ST) + G::kImg, wave);                            \
+        }                                                                                                        \
+    }
+    uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + 4 * G::kStage);
+#define SA_RING_STAMP(T, E)                                                                                      \
+    if (TIMING && blockIdx.x == 0 && lane == 0 && (T) >= 32 && (T) < 40)                                         \
+        stamp[(wave * 8 + ((T) - 32)) * 5 + (E)] = __builtin_amdgcn_s_memtime();
+    // k-step T in slot SLOT with fragments (FA, FB); next fragments into (NA, NB)
+#define SA_RING_STEP(SLOT, T, FA, FB, NA, NB)                                                                   \
+    {                                                                                                           \
+        SA_RING_STAMP(T, 0)                                                                                     \
+        const int sa_ = soff_a((T) + 4), sb_ = soff_b((T) + 4);                                                 \
+        char* st_ = smem + (SLOT) * G::kStage;                                                                  \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
+                mfma16_acc(acc[i][j], FB[j], FA[i]);                                                            \
+                const int m_ = i * 8 + j;                                                                       \
+                if (SCHED == 0) {                                                                               \
+                    if (m_ % 3 == 2 && m_ < 48) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ / 3)                  \
+                    if ((m_ & 7) == 7) SA_RING_PIECE(m_ >> 3, SLOT, sa_, sb_, st_)                              \
+                } else if (SCHED == 1) {                                                                        \
+                    if ((m_ & 1) == 1 && m_ < 32) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 1)               \
+                    if ((m_ & 3) == 3 && m_ >= 32) SA_RING_PIECE((m_ - 32) >> 2, SLOT, sa_, sb_, st_)           \
+                } else if (SCHED == 3) {                                                                        \
+                    if ((m_ & 1) == 1 && m_ < 32) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 1)               \
+                    if ((m_ & 1) == 1 && m_ >= 32 && m_ < 48) SA_RING_PIECE((m_ - 32) >> 1, SLOT, sa_, sb_, st_) \
+                } else {                                                                                        \
+                    if ((m_ & 3) == 1) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 2)                          \
+                    if ((m_ & 7) == 3) SA_RING_PIECE(m_ >> 3, SLOT, sa_, sb_, st_)                              \
+                }                                                                                               \
+            }                                                                                                   \
+        SA_RING_STAMP(T, 1)                                                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
+        SA_RING_STAMP(T, 2)                                                                                     \
+        wait_vm<4 * NP>();                                                                                      \
+        SA_RING_STAMP(T, 3)                                                                                     \
+        hard_barrier();                                                                                         \
+        SA_RING_STAMP(T, 4)                                                                                     \
+    }
+
+    // prologue: k-steps 0-3 in flight (clamped: a short block re-stages its last k-step), 0 and 1 landed, F_0 read,
+    // then a barrier so slot 0 may be restaged during k-step 0
+    stage_all(0, 0);
+    stage_all(1, 1);
+    stage_all(2, 2);
+    stage_all(3, 3);
+    wait_vm<4 * NP>();
+    hard_barrier();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) SA_RING_READ(0, fa0, fb0, f)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    hard_barrier();
+    int t = 0;
+    for (; t + 3 < ns; t += 4) {
+        SA_RING_STEP(0, t, fa0, fb0, fa1, fb1)
+        SA_RING_STEP(1, t + 1, fa1, fb1, fa0, fb0)
+        SA_RING_STEP(2, t + 2, fa0, fb0, fa1, fb1)
+        SA_RING_STEP(3, t + 3, fa1, fb1, fa0, fb0)
+    }
+    // no remainder: the dispatcher gives this kernel whole pairs of 64-deep tiles per block (ns % 4 == 0)
+#undef SA_RING_STEP
+#undef SA_RING_READ
+#undef SA_RING_PIECE
+#undef SA_RING_STAMP
+    wait_vm<0>();
+    if (TIMING && blockIdx.x == 0) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 4 * 8 * 5; i += blockDim.x) dbg[i] = stamp[i];
+    }
+    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    // epilogue: acc[i][j][e] = C[m0 + 128wm + 16i + (lane & 15)][n0 + 128wn + 16j + 4(lane >> 4) + e]
+    const int r = lane & 15, q4 = 4 * (lane >> 4);
+    if (unit >= 0) {  // K-slice of a tail tile: fp32 partial [256][256] at ws + unit * 65536
+        float* wp = ws + (int64_t)unit * 65536;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float* rp = wp + (128 * wm + 16 * i + r) * 256 + 128 * wn + q4;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4*>(rp + 16 * j) = acc[i][j];
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ldc + n0 + 128 * wn + q4;
+        u16x4 old[8];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = acc[i][j][e];
+                if (BETA) x += bf2f(old[j][e]);
+                o[e] = f2bf(x);
+            }
+            *reinterpret_cast<u16x4*>(crow_p + 16 * j) = o;
+        }
+    }
+}
+#define SA_RING_INST(BETA, SCHED, FD, TM)                                                                        \
+    template __global__ void gemm_tn_ring_kernel<BETA, SCHED, FD, TM>(                                           \
+        const u16* __restrict__, int, uint32_t, const u16* __restrict__, int, uint32_t, u16* __restrict__, int, int, \
+        int, int, int, int, float* __restrict__, uint64_t* __restrict__);
+#define SA_RING_INST2(SCHED, FD) SA_RING_INST(true, SCHED, FD, false) SA_RING_INST(false, SCHED, FD, false) \
+    SA_RING_INST(false, SCHED, FD, true)
+SA_RING_INST2(0, 0) SA_RING_INST2(1, 1) SA_RING_INST2(1, 2) SA_RING_INST2(3, 2) SA_RING_INST2(2, 2)
+#undef SA_RING_INST2
+#undef SA_RING_INST
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -1237,6 +1473,21 @@ void launch_tn_w4m16(const void* A, int64_t lda, const void* B, int64_t ldb, voi
                            (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
 }
 
+template <bool BETA, int SCHED, int FD>
+void launch_tn_ring(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
+                    int64_t N, int64_t K, hipStream_t st, int full_blocks, int split, float* ws) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
+    const int grid = full_blocks + (nwg - full_blocks) * split;
+    const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
+    hipLaunchKernelGGL((gemm_tn_ring_kernel<BETA, SCHED, FD, false>), dim3(grid), dim3(256), 4 * Cfg<32>::kStage, st,
+                       (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
+                       (int)K, full_blocks, split, ws, nullptr);
+    if (split > 1)
+        hipLaunchKernelGGL(gemm_tn_combine_kernel, dim3(nwg - full_blocks, 64), dim3(256), 0, st, (const float*)ws, (u16*)C,
+                           (int)ldc, (int)M, (int)N, full_blocks, split, BETA ? 1 : 0);
+}
+
 template <bool BETA, int BK, int STAGES, bool LW>
 void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                int64_t K, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr) {
@@ -1257,19 +1508,32 @@ void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, 
 using namespace sa_gemm;
 
 namespace sa_launch {
-// pipeline variants (benchmarking hook): 2 (default) = BK 64 x 2 stages, split staging (one 32-MFMA block per
+// pipeline variants (benchmarking hook): 10 (default) = four-slot ring, one wave per SIMD (gemm_tn_ring_kernel);
+// 9 / 11-13 = the ring with other schedules / LDS-DMA issue forms; 8 = one wave per SIMD on two 64-deep stages;
+// 2 = BK 64 x 2 stages, split staging (one 32-MFMA block per
 // phase); 5 = the same with three B buffers (B staged in group 1's read window); 0 = BK 32 x 4 stages, wait behind
 // the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2;
 // 6 = no ping-pong, reads interleaved with each wave's own MFMAs (gemm_tn_il_kernel); 7 = one wave per SIMD,
 // 128x128 wave tiles, register-staged (gemm_tn_w4_kernel)
-static int g_gemm_variant = 2;
+static int g_gemm_variant = 10;
 void gemm_set_variant(int v) { g_gemm_variant = v; }
+int gemm_get_variant() { return g_gemm_variant; }
 // profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
 void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                     int64_t K, uint64_t* dbg, hipStream_t st) {
     const int nwg = (int)((M / 256) * (N / 256));
     const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
     const int extra = kWaves * kDbgTiles * kDbgEv * 8;
+#define SA_RING_T(SCHED, FD)                                                                                    \
+    hipLaunchKernelGGL((gemm_tn_ring_kernel<false, SCHED, FD, true>), dim3(nwg), dim3(256), 4 * Cfg<32>::kStage + 4096, \
+                       st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, \
+                       (int)K, nwg, 1, nullptr, dbg);
+    if (g_gemm_variant == 9) { SA_RING_T(0, 0) return; }
+    if (g_gemm_variant == 10) { SA_RING_T(1, 1) return; }
+    if (g_gemm_variant == 11) { SA_RING_T(1, 2) return; }
+    if (g_gemm_variant == 12) { SA_RING_T(3, 2) return; }
+    if (g_gemm_variant == 13) { SA_RING_T(2, 2) return; }
+#undef SA_RING_T
     if (g_gemm_variant == 6)
         hipLaunchKernelGGL((gemm_tn_il_kernel<false, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra, st,
                            (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N,
@@ -1298,7 +1562,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     full_blocks = nwg;
     split = 1;
     if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6 && g_gemm_variant != 7 &&
-         g_gemm_variant != 8) ||
+         g_gemm_variant != 8 && (g_gemm_variant < 9 || g_gemm_variant > 13)) ||
         slots <= 0)
         return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
@@ -1306,8 +1570,10 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
     int s = 1;
     double best = 1.0;
+    const bool ring = g_gemm_variant >= 9 && g_gemm_variant <= 13;
+    if (ring && nk % 2 != 0) return 0;  // the ring kernels run whole pairs of 64-deep tiles (gemm_tn falls back)
     for (int c = 2; c <= 4; ++c) {
-        if (nk % c != 0 || nk / c < 4) continue;
+        if (nk % c != 0 || nk / c < 4 || (ring && (nk / c) % 2 != 0)) continue;
         const double cost = (double)((r * c + slots - 1) / slots) / c;
         if (cost < best - 1e-9) { best = cost; s = c; }
     }
@@ -1318,27 +1584,44 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
 }
 void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
              int64_t K, bool beta, hipStream_t st, int full_blocks, int split, float* ws) {
-    if (g_gemm_variant == 2 && split > 1) {
+    // the ring kernels (9-13) take whole pairs of 64-deep tiles per block only (K % 128): anything else runs variant 2
+    int v = g_gemm_variant;
+    if (v >= 9 && v <= 13 && (K / 64) % 2 != 0) v = 2;
+    if (v == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
-    if (g_gemm_variant == 8) {
+    if (v >= 9 && v <= 13) {
+#define SA_RING(SCHED, FD)                                                                                 \
+    if (beta) launch_tn_ring<true, SCHED, FD>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws); \
+    else launch_tn_ring<false, SCHED, FD>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
+        switch (v) {
+            case 9: SA_RING(0, 0) break;
+            case 10: SA_RING(1, 1) break;
+            case 11: SA_RING(1, 2) break;
+            case 12: SA_RING(3, 2) break;
+            default: SA_RING(2, 2) break;
+        }
+#undef SA_RING
+        return;
+    }
+    if (v == 8) {
         if (beta) launch_tn_w4m16<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn_w4m16<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
-    if (g_gemm_variant == 7) {
+    if (v == 7) {
         if (beta) launch_tn_w4<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn_w4<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
-    if (g_gemm_variant == 6) {
+    if (v == 6) {
         if (beta) launch_tn_il<true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn_il<false>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
-    if (g_gemm_variant == 5) {
+    if (v == 5) {
         if (beta) launch_tn<true, 64, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
@@ -1346,7 +1629,7 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
 #define SA_TN(BK, S, LW)                                                                      \
     if (beta) launch_tn<true, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);                \
     else launch_tn<false, BK, S, LW>(A, lda, B, ldb, C, ldc, M, N, K, st);
-    if (g_gemm_variant == 4) {
+    if (v == 4) {
         const int nwg = (int)((M / 256) * (N / 256));
         const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);
         if (beta)
@@ -1357,7 +1640,7 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
                                (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K);
         return;
     }
-    switch (g_gemm_variant) {
+    switch (v) {
         case 1: SA_TN(32, 4, false) break;
         case 2: SA_TN(64, 2, true) break;
         case 3: SA_TN(32, 5, true) break;

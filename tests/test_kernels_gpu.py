@@ -485,18 +485,20 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (1024, 512, 1024)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (512, 768, 384), (1024, 512, 1024)])
 def test_gemm_tn(M, N, K, accumulate, variant):
     """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands; pipeline
-    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers), 6 (no ping-pong) and 7 (one wave per
-    SIMD, register-staged)."""
+    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers), 6 (no ping-pong), 7 (one wave per
+    SIMD, register-staged), 8 (one wave per SIMD, two LDS-DMA stages) and the four-slot ring 9-12 (10 is the
+    default; K = 320 is an odd number of 64-deep tiles, which the ring hands to variant 2)."""
+    prev = ext().gemm_get_variant()
     ext().gemm_set_variant(variant)
     try:
         _gemm_tn_case(M, N, K, accumulate)
     finally:
-        ext().gemm_set_variant(2)
+        ext().gemm_set_variant(prev)
 
 
 def _gemm_tn_case(M, N, K, accumulate):

@@ -36,6 +36,7 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=5, help="interleaved timing rounds per variant (median reported)")
     a = ap.parse_args()
     T = a.tokens
+    default_variant = ext().gemm_get_variant()
     out = {}
     for name, (Nout, Kin) in SHAPES.items():
         g = torch.randn(T, Nout, device="cuda", dtype=torch.bfloat16)
@@ -65,7 +66,7 @@ def main() -> None:
                 samples[vv].append(fl / timeit(lambda: ext().gemm_tn(g, x, c, True), a.iters) / 1e12)
         for vv in vs:
             r[f"v{vv}"] = sorted(samples[vv])[len(samples[vv]) // 2]
-        ext().gemm_set_variant(2)
+        ext().gemm_set_variant(default_variant)
         r.update({
             "ours": fl / timeit(lambda: ext().gemm_tn(g, x, c, False), a.iters) / 1e12,
             "ours_acc": fl / timeit(lambda: ext().gemm_tn(g, x, c, True), a.iters) / 1e12,
