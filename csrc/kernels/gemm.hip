@@ -1162,7 +1162,9 @@ template __global__ void gemm_tn_w4m16_kernel<false>(const u16* __restrict__, in
 //  * one barrier per k-step: every wave's reads of slot (t+1)%4 retired and k-step t+2 landed (vmcnt leaves the
 //    16 pieces of k-steps t+3 and t+4 in flight), so each piece has 2-3 k-steps (2-3k cycles) to land instead of 1-2.
 //  SCHED: 0 = F_{t+1} reads one per 3 MFMAs over the first 48, pieces one per 8 MFMAs; 1 = reads one per 2 MFMAs over
-//  the first 32, pieces one per 4 over the last 32; 2 = reads one per 4 MFMAs, pieces one per 8 (offset by 4).
+//  the first 32, pieces one per 4 over the last 32; 2 = one fragment (two transposing reads) per 4 MFMAs and one piece
+//  per 8 over the whole k-step (the default: every issue slot evenly loaded, +2-4 % over 1); 5 = like 2 with the two
+//  reads of a fragment in separate MFMA gaps.
 //  FASTDMA: 0 = Dma::load_piece_nc (descriptor rebuilt per piece, m0 saved / restored); 1 = descriptors built once,
 //  m0 clobbered (the compiler emits no other m0 use in this kernel, but an m0 clobber is only a warning to it);
 //  2 = descriptors built once, m0 saved / restored around each piece.
@@ -1243,6 +1245,22 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
         if ((F) < 8) FB[(F)] = frag(ob[(SLOT) >> 1][(F)], (SLOT));            \
         else FA[(F) - 8] = frag(oa[(SLOT) >> 1][(F) - 8], (SLOT));            \
     }
+    // one of the two transposing reads of fragment F (H = 0: k rows 0-15 half, 1: the +16 rows half), written into
+    // that half of the fragment register in place
+    auto half = [&](int off, int slot, int h) -> s16x4 {
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + off + (slot & 1) * G::kStage + h * 16 * 512));
+    };
+#define SA_RING_HALF(SLOT, FA, FB, F, H)                                                                        \
+    {                                                                                                           \
+        bf16x8& d_ = (F) < 8 ? FB[(F)] : FA[(F) - 8];                                                           \
+        const s16x4 x_ = half((F) < 8 ? ob[(SLOT) >> 1][(F)] : oa[(SLOT) >> 1][(F) - 8], (SLOT), (H));          \
+        s16x8 w_ = __builtin_bit_cast(s16x8, d_);                                                               \
+        if ((H) == 0) w_ = __builtin_shufflevector(w_, __builtin_shufflevector(x_, x_, 0, 1, 2, 3, 0, 1, 2, 3), \
+                                                   8, 9, 10, 11, 4, 5, 6, 7);                                   \
+        else w_ = __builtin_shufflevector(w_, __builtin_shufflevector(x_, x_, 0, 1, 2, 3, 0, 1, 2, 3),          \
+                                          0, 1, 2, 3, 8, 9, 10, 11);                                            \
+        d_ = __builtin_bit_cast(bf16x8, w_);                                                                    \
+    }
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     const i32x4 rsa = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(A)),
                        (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(A) >> 32)) & 0xffff),
@@ -1301,9 +1319,12 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
                 } else if (SCHED == 3) {                                                                        \
                     if ((m_ & 1) == 1 && m_ < 32) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 1)               \
                     if ((m_ & 1) == 1 && m_ >= 32 && m_ < 48) SA_RING_PIECE((m_ - 32) >> 1, SLOT, sa_, sb_, st_) \
-                } else {                                                                                        \
+                } else if (SCHED == 2) {                                                                        \
                     if ((m_ & 3) == 1) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 2)                          \
                     if ((m_ & 7) == 3) SA_RING_PIECE(m_ >> 3, SLOT, sa_, sb_, st_)                              \
+                } else {                                                                                        \
+                    if ((m_ & 1) == 0) SA_RING_HALF(((SLOT) + 1) & 3, NA, NB, m_ >> 2, (m_ >> 1) & 1)           \
+                    if ((m_ & 7) == 5) SA_RING_PIECE(m_ >> 3, SLOT, sa_, sb_, st_)                              \
                 }                                                                                               \
             }                                                                                                   \
         SA_RING_STAMP(T, 1)                                                                                     \
@@ -1337,6 +1358,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
     // no remainder: the dispatcher gives this kernel whole pairs of 64-deep tiles per block (ns % 4 == 0)
 #undef SA_RING_STEP
 #undef SA_RING_READ
+#undef SA_RING_HALF
 #undef SA_RING_PIECE
 #undef SA_RING_STAMP
     wait_vm<0>();
@@ -1386,7 +1408,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
         int, int, int, int, float* __restrict__, uint64_t* __restrict__);
 #define SA_RING_INST2(SCHED, FD) SA_RING_INST(true, SCHED, FD, false) SA_RING_INST(false, SCHED, FD, false) \
     SA_RING_INST(false, SCHED, FD, true)
-SA_RING_INST2(0, 0) SA_RING_INST2(1, 1) SA_RING_INST2(1, 2) SA_RING_INST2(3, 2) SA_RING_INST2(2, 2)
+SA_RING_INST2(0, 0) SA_RING_INST2(1, 1) SA_RING_INST2(1, 2) SA_RING_INST2(3, 2) SA_RING_INST2(2, 1)
+SA_RING_INST2(5, 1)
 #undef SA_RING_INST2
 #undef SA_RING_INST
 
@@ -1508,14 +1531,15 @@ void launch_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, 
 using namespace sa_gemm;
 
 namespace sa_launch {
-// pipeline variants (benchmarking hook): 10 (default) = four-slot ring, one wave per SIMD (gemm_tn_ring_kernel);
-// 9 / 11-13 = the ring with other schedules / LDS-DMA issue forms; 8 = one wave per SIMD on two 64-deep stages;
+// pipeline variants (benchmarking hook): 13 (default) = four-slot ring, one wave per SIMD (gemm_tn_ring_kernel) with
+// fragment reads and LDS-DMA pieces spread over the whole k-step; 9-12 / 14 = the ring with other schedules / LDS-DMA
+// issue forms (profiles/gemm_ring_variants_r3*.log); 8 = one wave per SIMD on two 64-deep stages;
 // 2 = BK 64 x 2 stages, split staging (one 32-MFMA block per
 // phase); 5 = the same with three B buffers (B staged in group 1's read window); 0 = BK 32 x 4 stages, wait behind
 // the MFMAs; 1 = same, wait before the first barrier; 3 = BK 32 x 5 stages; 4 = 16x16x32 MFMA form of 2;
 // 6 = no ping-pong, reads interleaved with each wave's own MFMAs (gemm_tn_il_kernel); 7 = one wave per SIMD,
 // 128x128 wave tiles, register-staged (gemm_tn_w4_kernel)
-static int g_gemm_variant = 10;
+static int g_gemm_variant = 13;
 void gemm_set_variant(int v) { g_gemm_variant = v; }
 int gemm_get_variant() { return g_gemm_variant; }
 // profiling hook: one launch of the timing build (variant 0 or 2), stamps of workgroup 0 to dbg (8 x 8 x 5 uint64)
@@ -1532,7 +1556,8 @@ void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void
     if (g_gemm_variant == 10) { SA_RING_T(1, 1) return; }
     if (g_gemm_variant == 11) { SA_RING_T(1, 2) return; }
     if (g_gemm_variant == 12) { SA_RING_T(3, 2) return; }
-    if (g_gemm_variant == 13) { SA_RING_T(2, 2) return; }
+    if (g_gemm_variant == 13) { SA_RING_T(2, 1) return; }
+    if (g_gemm_variant == 14) { SA_RING_T(5, 1) return; }
 #undef SA_RING_T
     if (g_gemm_variant == 6)
         hipLaunchKernelGGL((gemm_tn_il_kernel<false, true>), dim3(nwg), dim3(512), 2 * Cfg<64>::kStage + extra, st,
@@ -1562,7 +1587,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     full_blocks = nwg;
     split = 1;
     if ((g_gemm_variant != 2 && g_gemm_variant != 5 && g_gemm_variant != 6 && g_gemm_variant != 7 &&
-         g_gemm_variant != 8 && (g_gemm_variant < 9 || g_gemm_variant > 13)) ||
+         g_gemm_variant != 8 && (g_gemm_variant < 9 || g_gemm_variant > 14)) ||
         slots <= 0)
         return 0;
     const int r = nwg % slots, nk = (int)(K / 64);
@@ -1570,7 +1595,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
     // the split tail costs ceil(r * s / slots) rounds of 1/s of a tile: pick the cheapest s (fewest on ties)
     int s = 1;
     double best = 1.0;
-    const bool ring = g_gemm_variant >= 9 && g_gemm_variant <= 13;
+    const bool ring = g_gemm_variant >= 9 && g_gemm_variant <= 14;
     if (ring && nk % 2 != 0) return 0;  // the ring kernels run whole pairs of 64-deep tiles (gemm_tn falls back)
     for (int c = 2; c <= 4; ++c) {
         if (nk % c != 0 || nk / c < 4 || (ring && (nk / c) % 2 != 0)) continue;
@@ -1586,13 +1611,13 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
              int64_t K, bool beta, hipStream_t st, int full_blocks, int split, float* ws) {
     // the ring kernels (9-13) take whole pairs of 64-deep tiles per block only (K % 128): anything else runs variant 2
     int v = g_gemm_variant;
-    if (v >= 9 && v <= 13 && (K / 64) % 2 != 0) v = 2;
+    if (v >= 9 && v <= 14 && (K / 64) % 2 != 0) v = 2;
     if (v == 2 && split > 1) {
         if (beta) launch_tn<true, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         else launch_tn<false, 64, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
         return;
     }
-    if (v >= 9 && v <= 13) {
+    if (v >= 9 && v <= 14) {
 #define SA_RING(SCHED, FD)                                                                                 \
     if (beta) launch_tn_ring<true, SCHED, FD>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws); \
     else launch_tn_ring<false, SCHED, FD>(A, lda, B, ldb, C, ldc, M, N, K, st, full_blocks, split, ws);
@@ -1601,7 +1626,8 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
             case 10: SA_RING(1, 1) break;
             case 11: SA_RING(1, 2) break;
             case 12: SA_RING(3, 2) break;
-            default: SA_RING(2, 2) break;
+            case 13: SA_RING(2, 1) break;
+            default: SA_RING(5, 1) break;
         }
 #undef SA_RING
         return;

@@ -485,7 +485,7 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (512, 768, 384), (1024, 512, 1024)])
 def test_gemm_tn(M, N, K, accumulate, variant):
