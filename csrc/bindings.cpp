@@ -413,6 +413,35 @@ void gemm_tn(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool
                        ws_floats > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
+// C[M, N] = A B^T (+ C if accumulate); A: [M, K], B: [N, K] (a linear layer's weight), C: [M, N], bf16, unit inner
+// strides (the forward / input-gradient GEMM of a linear layer)
+bool gemm_nt_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+    if (!(A.is_cuda() && B.is_cuda() && C.is_cuda() && A.dim() == 2 && B.dim() == 2 && C.dim() == 2)) return false;
+    if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16 || C.scalar_type() != at::kBFloat16)
+        return false;
+    if (A.stride(1) != 1 || B.stride(1) != 1 || C.stride(1) != 1 || A.size(1) != B.size(1) || C.size(0) != A.size(0) ||
+        C.size(1) != B.size(0))
+        return false;
+    for (const at::Tensor* t : {&A, &B}) if ((uintptr_t)t->data_ptr() % 16 != 0) return false;
+    if ((uintptr_t)C.data_ptr() % 8 != 0) return false;
+    return sa_launch::gemm_nt_supported(A.size(0), B.size(0), A.size(1), A.stride(0), B.stride(0), C.stride(0));
+}
+void gemm_nt(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool accumulate) {
+    TORCH_CHECK(gemm_nt_ok(A, B, C), "gemm_nt: unsupported operands (bf16 2-D, M/N multiple of 256, K of 128)");
+    const at::DeviceGuard g(A.device());
+    sa_launch::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), A.size(0),
+                       B.size(0), A.size(1), accumulate, cur_stream());
+}
+
+at::Tensor gemm_nt_timing(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
+    TORCH_CHECK(gemm_nt_ok(A, B, C) && A.size(1) >= 32 * 40, "gemm_nt_timing: unsupported operands");
+    const at::DeviceGuard g(A.device());
+    auto dbg = at::zeros({4 * 8 * 5}, A.options().dtype(at::kLong));
+    sa_launch::gemm_nt(A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), C.data_ptr(), C.stride(0), A.size(0),
+                       B.size(0), A.size(1), false, cur_stream(), (uint64_t*)dbg.data_ptr());
+    return dbg;
+}
+
 at::Tensor gemm_tn_timing(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
     TORCH_CHECK(gemm_tn_ok(A, B, C) && A.size(0) >= 32 * 72, "gemm_tn_timing: unsupported operands");
     const at::DeviceGuard g(A.device());
@@ -621,6 +650,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
     m.def("gemm_set_variant", &sa_launch::gemm_set_variant, "select the gemm_tn pipeline variant (benchmarking)");
     m.def("gemm_get_variant", &sa_launch::gemm_get_variant, "the current gemm_tn pipeline variant");
+    m.def("gemm_nt_ok", &gemm_nt_ok, "whether gemm_nt supports these operands");
+    m.def("gemm_nt", &gemm_nt, "C (+)= A @ B^T (bf16, k-contiguous operands, HIP ring kernel)");
+    m.def("gemm_nt_timing", &gemm_nt_timing, "profiling: per-k-step s_memtime stamps of gemm_nt workgroup 0");
     m.def("gemm_tn_timing", &gemm_tn_timing, "profiling: per-phase s_memtime stamps of gemm_tn workgroup 0");
     m.def("ar_alloc", &ar_alloc, "one-shot all-reduce: allocate + IPC-export a registered buffer");
     m.def("ar_open", &ar_open, "one-shot all-reduce: map a peer's registered buffer");

@@ -1413,6 +1413,184 @@ SA_RING_INST2(5, 1)
 #undef SA_RING_INST2
 #undef SA_RING_INST
 
+// ---------------------------------------------------------------------------------------------------------------
+// Forward / input-gradient GEMM  C[M, N] (+)= A[M, K] B[N, K]^T  with both operands k-contiguous (row-major A, and B
+// stored [N][K]: a linear layer's weight for the forward, its cached transpose for dgrad) on the wgrad ring's
+// structure: 256x256 macro tile, 4 waves x 128x128 (16x16x32 MFMAs, in-place AGPR accumulators), four-slot LDS ring of
+// 32-deep k-steps filled by LDS-DMA, one barrier per k-step.  Here the operand rows are k-contiguous, so a fragment
+// (row l & 15, k 8(l >> 4) .. +7) is ONE ds_read_b128 instead of two transposing reads.
+//  * image per operand and slot: [256 rows][32 k] bf16, 64-B rows; the 16-B chunk c of row r sits at chunk
+//    c ^ f(r), f = (-(r >> 2)) & 3, which makes every ds_read_b128 lane group of a fragment read hit 16 distinct
+//    16-B bank windows (conflict-free);
+//  * LDS-DMA piece = 16 rows x 64 B; the source is permuted so the lane-linear destination is the swizzled image;
+//  * all fragment addresses are one per-lane VGPR per slot pair + a compile-time immediate.
+__device__ __forceinline__ int nt_sw(int r) { return (-(r >> 2)) & 3; }
+
+template <bool BETA, bool TIMING = false>
+__global__ __launch_bounds__(256, 1) void gemm_nt_ring_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                              const u16* __restrict__ B, int ldb, uint32_t b_bytes,
+                                                              u16* __restrict__ C, int ldc, int M, int N, int K,
+                                                              uint64_t* __restrict__ dbg = nullptr) {
+    constexpr int BK = 32, IMG = 256 * BK * 2, STAGE = 2 * IMG;  // 16 KiB per image, 32 KiB per slot
+    constexpr int NW = 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tm = M / 256, tn = N / 256, nwg = tm * tn;
+    const int v = xcd_remap(blockIdx.x, nwg);
+    const int group = kGroupM * tn;
+    const int first_m = (v / group) * kGroupM;
+    const int gm = min(tm - first_m, kGroupM);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
+    const int ns = K / BK;
+
+    // DMA: lane -> (row lane >> 2 of the piece, chunk slot lane & 3), source chunk = slot ^ f(row); piece i of this
+    // wave covers rows 16 (wave + 4 i) .. +15 (f depends on row & 15 only: piece-invariant)
+    const int prow = lane >> 2, pchunk = (lane & 3) ^ nt_sw(prow);
+    const int va = ((16 * wave + prow) * lda + 8 * pchunk) * 2;
+    const int vb = ((16 * wave + prow) * ldb + 8 * pchunk) * 2;
+    const int stepa = __builtin_amdgcn_readfirstlane(64 * lda * 2), stepb = __builtin_amdgcn_readfirstlane(64 * ldb * 2);
+    const int basea = __builtin_amdgcn_readfirstlane(m0 * lda * 2), baseb = __builtin_amdgcn_readfirstlane(n0 * ldb * 2);
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 rsa = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(A)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(A) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(a_bytes), fa::kBufFlags};
+    const i32x4 rsb = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(B)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(B) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(b_bytes), fa::kBufFlags};
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)smem));
+    // piece P (even: A piece P/2, odd: B piece P/2) of k-step U into slot SLOT.  m0 is written in the statement that
+    // reads it (the compiler emits no other m0 use in this kernel; its clobber is only a warning to hipcc).
+#define SA_NT_PIECE(P, SLOT, U)                                                                                     \
+    {                                                                                                               \
+        const bool isb_ = ((P) & 1) != 0;                                                                           \
+        const int i_ = (P) >> 1;                                                                                    \
+        const uint32_t l_ = lds0 + (SLOT) * STAGE + (isb_ ? IMG : 0) + (wave + NW * i_) * 1024;                   \
+        const int ku_ = min((U), ns - 1) * BK * 2;                                                                  \
+        if (isb_)                                                                                                   \
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"                 \
+                         ::"s"(l_), "v"(vb), "s"(rsb), "s"(baseb + i_ * stepb + ku_) : "m0");                     \
+        else                                                                                                        \
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"                 \
+                         ::"s"(l_), "v"(va), "s"(rsa), "s"(basea + i_ * stepa + ku_) : "m0");                     \
+    }
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragment addresses: per-lane part + (slot pair) + wave rows; fragment i / slot parity in the immediate
+    int oa[2], ob[2];
+    {
+        const int r = lane & 15, g = lane >> 4;
+        const int lo = r * 64 + 16 * (g ^ nt_sw(r));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            oa[h] = h * 2 * STAGE + 128 * wm * 64 + lo;
+            ob[h] = h * 2 * STAGE + IMG + 128 * wn * 64 + lo;
+            // opaque: otherwise hipcc rebuilds the slot-pair-1 bases as base + 0x1xxxx with a v_add per read
+            asm volatile("" : "+v"(oa[h]), "+v"(ob[h]));
+        }
+    }
+    auto frag = [&](int base, int slot, int i) -> bf16x8 {
+        return *reinterpret_cast<const bf16x8*>(smem + base + (slot & 1) * STAGE + i * 16 * 64);
+    };
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+#define SA_NT_READ(SLOT, FA, FB, F)                                                 \
+    {                                                                               \
+        if ((F) < 8) FB[(F)] = frag(ob[(SLOT) >> 1], (SLOT), (F));                  \
+        else FA[(F) - 8] = frag(oa[(SLOT) >> 1], (SLOT), (F) - 8);                  \
+    }
+    // k-step T in slot SLOT: MFMAs on (FA, FB), next fragments into (NA, NB) one per 4 MFMAs, k-step T+4's pieces
+    // into slot SLOT one per 8 MFMAs; then every read of the next slot retired, k-step T+2 landed, barrier
+    uint64_t* stamp = reinterpret_cast<uint64_t*>(smem + 4 * STAGE);
+#define SA_NT_STAMP(T, E)                                                                                        \
+    if (TIMING && blockIdx.x == 0 && lane == 0 && (T) >= 32 && (T) < 40)                                         \
+        stamp[(wave * 8 + ((T) - 32)) * 5 + (E)] = __builtin_amdgcn_s_memtime();
+#define SA_NT_STEP(SLOT, T, FA, FB, NA, NB)                                                                     \
+    {                                                                                                           \
+        SA_NT_STAMP(T, 0)                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
+                mfma16_acc(acc[i][j], FB[j], FA[i]);                                                            \
+                const int m_ = i * 8 + j;                                                                       \
+                if ((m_ & 3) == 1) SA_NT_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 2)                                \
+                if ((m_ & 7) == 3) SA_NT_PIECE(m_ >> 3, SLOT, (T) + 4)                                          \
+            }                                                                                                   \
+        SA_NT_STAMP(T, 1)                                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
+        SA_NT_STAMP(T, 2)                                                                                       \
+        wait_vm<16>();                                                                                          \
+        SA_NT_STAMP(T, 3)                                                                                       \
+        hard_barrier();                                                                                         \
+        SA_NT_STAMP(T, 4)                                                                                       \
+    }
+
+    // prologue: k-steps 0-3 in flight, 0 and 1 landed, F_0 read, then a barrier (slot 0 is restaged in k-step 0)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) SA_NT_PIECE(p, u, u)
+    wait_vm<16>();
+    hard_barrier();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) SA_NT_READ(0, fa0, fb0, f)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    hard_barrier();
+    for (int t = 0; t < ns; t += 4) {  // ns % 4 == 0 (the dispatcher checks K % 128)
+        SA_NT_STEP(0, t, fa0, fb0, fa1, fb1)
+        SA_NT_STEP(1, t + 1, fa1, fb1, fa0, fb0)
+        SA_NT_STEP(2, t + 2, fa0, fb0, fa1, fb1)
+        SA_NT_STEP(3, t + 3, fa1, fb1, fa0, fb0)
+    }
+#undef SA_NT_STEP
+#undef SA_NT_READ
+#undef SA_NT_PIECE
+#undef SA_NT_STAMP
+    wait_vm<0>();
+    if (TIMING && blockIdx.x == 0) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 4 * 8 * 5; i += blockDim.x) dbg[i] = stamp[i];
+    }
+    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    // epilogue: acc[i][j][e] = C[m0 + 128wm + 16i + (lane & 15)][n0 + 128wn + 16j + 4(lane >> 4) + e]
+    const int r = lane & 15, q4 = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        u16* crow_p = C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ldc + n0 + 128 * wn + q4;
+        u16x4 old[8];
+        if (BETA) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            u16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = acc[i][j][e];
+                if (BETA) x += bf2f(old[j][e]);
+                o[e] = f2bf(x);
+            }
+            *reinterpret_cast<u16x4*>(crow_p + 16 * j) = o;
+        }
+    }
+}
+template __global__ void gemm_nt_ring_kernel<true, false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                          int, uint32_t, u16* __restrict__, int, int, int, int,
+                                                          uint64_t* __restrict__);
+template __global__ void gemm_nt_ring_kernel<false, false>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                           int, uint32_t, u16* __restrict__, int, int, int, int,
+                                                           uint64_t* __restrict__);
+template __global__ void gemm_nt_ring_kernel<false, true>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                          int, uint32_t, u16* __restrict__, int, int, int, int,
+                                                          uint64_t* __restrict__);
+
 // explicit instantiations: hipcc otherwise silently drops the host stubs of some instances of this kernel
 // template (the build's stub check catches that)
 #define SA_GEMM_INST(BETA, BK, S, LW, TM)                                                                          \
@@ -1673,5 +1851,24 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
         default: SA_TN(32, 4, true) break;
     }
 #undef SA_TN
+}
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
+    return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+           ldc % 4 == 0 && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
+           (M / 256) * (N / 256) < (int64_t(1) << 31) && ldc < (1 << 30);
+}
+void gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, bool beta, hipStream_t st, uint64_t* timing_dbg) {
+    const int nwg = (int)((M / 256) * (N / 256));
+    const uint32_t ab = (uint32_t)(M * lda * 2), bb = (uint32_t)(N * ldb * 2);
+    if (timing_dbg)
+        hipLaunchKernelGGL((gemm_nt_ring_kernel<false, true>), dim3(nwg), dim3(256), 128 * 1024 + 4096, st, (const u16*)A,
+                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, timing_dbg);
+    else if (beta)
+        hipLaunchKernelGGL((gemm_nt_ring_kernel<true, false>), dim3(nwg), dim3(256), 128 * 1024, st, (const u16*)A,
+                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, nullptr);
+    else
+        hipLaunchKernelGGL((gemm_nt_ring_kernel<false, false>), dim3(nwg), dim3(256), 128 * 1024, st, (const u16*)A,
+                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (u16*)C, (int)ldc, (int)M, (int)N, (int)K, nullptr);
 }
 }  // namespace sa_launch

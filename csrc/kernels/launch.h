@@ -54,6 +54,9 @@ namespace sa_launch {
 // gemm.hip: C[M, N] (+)= A^T B, A [K, M] / B [K, N] row-major (k-major operands), bf16
 void gemm_set_variant(int v);
 int gemm_get_variant();
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+void gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, bool beta, hipStream_t st, uint64_t* timing_dbg = nullptr);
 void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
                     int64_t K, uint64_t* dbg, hipStream_t st);
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);

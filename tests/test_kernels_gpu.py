@@ -515,6 +515,25 @@ def _gemm_tn_case(M, N, K, accumulate):
     assert not ext().gemm_tn_ok(A[:, :200], B, C[:200])
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2)])
+def test_gemm_nt(M, N, K, accumulate):
+    """Forward / dgrad GEMM C (+)= A B^T (ring kernel, ds_read_b128 fragments) against an fp32 reference, with a
+    strided (sliced) A and an asymmetric B."""
+    torch.manual_seed(7)
+    A_full = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
+    A = A_full[:, 64:]
+    B = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * torch.linspace(0.5, 1.5, K, device=DEV).to(torch.bfloat16)
+    C0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    C = C0.clone()
+    assert ext().gemm_nt_ok(A, B, C)
+    ext().gemm_nt(A, B, C, accumulate)
+    ref = A.float() @ B.float().t() + (C0.float() if accumulate else 0)
+    torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
+    assert not ext().gemm_nt_ok(A[:200], B, C[:200])
+    assert not ext().gemm_nt_ok(A[:, : K - 64], B[:, : K - 64], C)
+
+
 # ---------------------------------------------------------------- masked softmax / activations / dropout
 from scaling_amd.ops import elementwise  # noqa: E402
 
