@@ -89,8 +89,11 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
 //   S = Q K^T, dP = dO V^T (row reads), p = exp2(S c - lse2), dS = p (dP - delta),
 //   dV^T += dO^T P, dK^T += Q^T dS (transposed reads; P / dS accumulators are the B operands).
 // Query rows past the segment arrive as zeros (Q = dO = 0, lse2 = delta = 0) and contribute nothing.
-template <int D, bool F16, bool DROP>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
+// OCC: waves per SIMD the register budget is sized for (1: the whole register file, with explicit read-ahead);
+// ADMA: the per-tile LDS-DMA as inline asm retired by an explicit vmcnt(0) before the barrier (compiler-visible
+// LDS-DMA makes hipcc wait for the NEXT tile's DMA in front of this tile's transposed LDS reads).
+template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false>
+__global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int QT = 32, TILE = QT * D * 2, BUF = 2 * TILE + 512, VIMG = 128 * D * 2, NKS = D / 16, NT = D / 32;
@@ -133,6 +136,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const u16* kp = a.k + (int64_t)(k0s + min(mykey, Lk - 1)) * a.k_tok + (int64_t)hk * a.k_head;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) kf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(kp + 16 * ks + 8 * h));
+        // consume K here: hipcc retires the loads before the tile loop (inside it its vmcnt would also wait for
+        // the asm LDS-DMA in flight)
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(kf[ks]));
     }
     LdsOffsets<D> lo;
     lo.init(lane);
@@ -143,13 +150,24 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     // incrementally (no runtime divisions in the loop)
     auto issue = [&](int gi, int qi, char* buf) {
         const int qt = qlo + qi * QT, hq = h0 + gi;
-        dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
-        dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
+        if constexpr (ADMA) {
+            dma_tile_asm(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
+            dma_tile_asm(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE,
+                         wave);
+        } else {
+            dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
+            dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
+        }
         if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
             const int64_t ix = (int64_t)hq * a.lse_stride + q0s + qt;
             const uint32_t nb = (uint32_t)max(min(QT, Lq - qt), 0) * 4u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
+            if constexpr (ADMA) {
+                dma_dword_asm(a.lse2 + ix, nb, 4 * lane, buf + 2 * TILE);
+                dma_dword_asm(a.delta + ix, nb, 4 * lane, buf + 2 * TILE + 256);
+            } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
+            }
         }
     };
     f32x16 dk[NT], dv[NT];
@@ -168,15 +186,41 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
                                (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
         f32x16 s = f32x16{}, dp = f32x16{};
+        if constexpr (OCC == 1) {
+            // one wave per SIMD: the register file has room to read PD k-steps ahead, so no MFMA waits on the LDS
+            // latency of its own operands
+            constexpr int PD = 3;
+            bf16x8 rq[PD], rdo[PD], rv[PD];
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            s = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], s);
-            dp = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dp);
-        }
+            for (int ks = 0; ks < PD; ++ks) {
+                rq[ks] = rd_row<D>(Q, 0, lo.row(ks));
+                rdo[ks] = rd_row<D>(DO, 0, lo.row(ks));
+                rv[ks] = rd_row<D>(vw_img, 0, lo.row(ks));
+            }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            for (int ks = 0; ks < NKS; ++ks) {
+                const int b = ks % PD;
+                s = mma<F16>(rq[b], kf[ks], s);
+                dp = mma<F16>(rdo[b], rv[b], dp);
+                if (ks + PD < NKS) {
+                    rq[b] = rd_row<D>(Q, 0, lo.row(ks + PD));
+                    rdo[b] = rd_row<D>(DO, 0, lo.row(ks + PD));
+                    rv[b] = rd_row<D>(vw_img, 0, lo.row(ks + PD));
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead: the scheduler would sink reads to their use
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                s = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], s);
+                dp = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dp);
+            }
+#pragma unroll
+            for (int i = 0; i < 2 * NKS; ++i) {  // bounded read-ahead keeps the register budget
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
         }
         // query of register j: qt + 4h + crow(j)
         int mlo = -1 << 30, mhi = 1 << 30;
@@ -216,20 +260,45 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 }
             }
         }
+        if constexpr (OCC == 1) {
+            const bf16x8 pb[2] = {pack_acc_t<F16>(s, 0), pack_acc_t<F16>(s, 1)};
+            const bf16x8 db[2] = {pack_acc_t<F16>(dp, 0), pack_acc_t<F16>(dp, 1)};
+            constexpr int NS = 2 * NT, PD = 3;  // steps (ss, t); fragments PD steps ahead
+            bf16x8 fo[PD], fq[PD];
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-            const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
-            const int kb = 16 * ss * D * 2;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                dv[t] = mma<F16>(rd_tr<D>(DO, kb, lo, t), pb, dv[t]);
-                dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo, t), db, dk[t]);
+            for (int i = 0; i < PD; ++i) {
+                fo[i] = rd_tr<D>(DO, 16 * (i / NT) * D * 2, lo, i % NT);
+                fq[i] = rd_tr<D>(Q, 16 * (i / NT) * D * 2, lo, i % NT);
             }
-        }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 4 * NT; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            for (int i = 0; i < NS; ++i) {
+                const int ss = i / NT, t = i % NT, b = i % PD;
+                dv[t] = mma<F16>(fo[b], pb[ss], dv[t]);
+                dk[t] = mma<F16>(fq[b], db[ss], dk[t]);
+                if (i + PD < NS) {
+                    const int j = i + PD;
+                    fo[b] = rd_tr<D>(DO, 16 * (j / NT) * D * 2, lo, j % NT);
+                    fq[b] = rd_tr<D>(Q, 16 * (j / NT) * D * 2, lo, j % NT);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
+                const int kb = 16 * ss * D * 2;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    dv[t] = mma<F16>(rd_tr<D>(DO, kb, lo, t), pb, dv[t]);
+                    dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo, t), db, dk[t]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            }
         }
     };
 
@@ -246,6 +315,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         issue(ig, iq, buf0);
         adv(ig, iq);
     }
+    if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int w = 0;
     for (; w + 1 < nwork; w += 2) {
@@ -253,6 +323,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         adv(ig, iq);
         tile(buf0, cg, cq);
         adv(cg, cq);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (w + 2 < nwork) {
             issue(ig, iq, buf0);
@@ -260,6 +331,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         }
         tile(buf1, cg, cq);
         adv(cg, cq);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     if (w < nwork) tile(buf0, cg, cq);
@@ -306,8 +378,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: workgroup = 4 waves x 32 queries of one (segment, q head); query on the lane (Q, dO rows are
 // register-resident B operands), K / V tiles of 64 keys double-buffered in LDS by LDS-DMA.  Per 32-key block:
 //   S^T = K Q^T, dP^T = V dO^T, p = exp2(S c - lse2), dS = p (dP - delta), dQ^T += K^T dS^T.
-template <int D, bool F16, bool DROP>
-__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
+template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false>
+__global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
@@ -345,6 +417,10 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     }
     const float nl2 = myq < Lq ? -a.lse[(int64_t)hq * a.lse_stride + q0s + myq] * 1.4426950408889634f : -INFINITY;
     const float dlt = myq < Lq ? a.delta[(int64_t)hq * a.lse_stride + q0s + myq] : 0.f;
+    // consume the register-resident operands here (their loads retire before the loop, see fa_bwd_dkdv_kernel)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) asm volatile("" ::"v"(qf[ks]), "v"(df[ks]));
+    asm volatile("" ::"v"(nl2), "v"(dlt));
     uint32_t drow = 0;
     if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
     LdsOffsets<D> lo;
@@ -356,10 +432,15 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
     // (DMA issued through the free function dma_load: a direct DmaTile::load call in this kernel makes
     //  hipcc's host pass treat the kernel as undefined and drop its launch stub)
-#define SA_DQ_ISSUE(KT, BUFP)                                                                 \
-    do {                                                                                      \
-        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);        \
-        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u); \
+#define SA_DQ_ISSUE(KT, BUFP)                                                                          \
+    do {                                                                                               \
+        if constexpr (ADMA) {                                                                          \
+            dma_tile_asm(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);        \
+            dma_tile_asm(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u); \
+        } else {                                                                                       \
+            dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);            \
+            dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u);     \
+        }                                                                                              \
     } while (0)
     f32x16 dq[NT];
 #pragma unroll
@@ -414,15 +495,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     char* buf0 = smem;
     char* buf1 = smem + 2 * TILE;
     if (klo < khi) SA_DQ_ISSUE(klo, buf0);
+    if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ntiles = khi > klo ? (khi - klo + 63) / 64 : 0;
     int kt = klo;
     for (int pr = 0; pr < ntiles / 2; ++pr, kt += 128) {
         SA_DQ_ISSUE(kt + 64, buf1);
         tile(buf0, kt);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (kt + 128 < khi) SA_DQ_ISSUE(kt + 128, buf0);
         tile(buf1, kt + 64);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     if (ntiles & 1) tile(buf0, kt);
@@ -470,19 +554,44 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
+// A/B switches (read once): SCALING_AMD_FA_BWD_OCC=1 -> one wave per SIMD with read-ahead; SCALING_AMD_FA_BWD_ADMA=1 ->
+// per-tile LDS-DMA as inline asm with its own vmcnt
+static int bwd_occ() {
+    static const int v = [] {
+        const char* e = getenv("SCALING_AMD_FA_BWD_OCC");
+        return e && atoi(e) == 1 ? 1 : 2;
+    }();
+    return v;
+}
+static bool bwd_adma() {
+    static const bool v = [] {
+        const char* e = getenv("SCALING_AMD_FA_BWD_ADMA");
+        return e && atoi(e) == 1;
+    }();
+    return v;
+}
+
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
-        if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        if (D == 128 && bwd_occ() == 1 && bwd_adma())
+            hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
+        else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
+        else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);
+        else if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     {
         dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
-        if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        if (D == 128 && bwd_occ() == 1 && bwd_adma())
+            hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
+        else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
+        else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);
+        else if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }

@@ -191,7 +191,9 @@ struct FwdV2 {
 
 // NW = 8: one 512-thread workgroup per CU; NW = 4: two independent 256-thread workgroups per CU (their phases
 // drift apart, so one workgroup's softmax can overlap the other's MFMAs on a SIMD)
-template <int D, bool F16, bool DROP, int NW = 8>
+// ADMA: the per-tile LDS-DMA as inline asm retired by an explicit vmcnt(0) before the barrier (with compiler-visible
+// LDS-DMA hipcc waits for the NEXT tile's DMA in front of this tile's transposed V reads)
+template <int D, bool F16, bool DROP, int NW = 8, bool ADMA = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     using C = FwdV2<D, NW>;
@@ -240,10 +242,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
     tv.init(wave_u, lane, a.v_tok);
     const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
-#define SA_FWD_ISSUE(KT, BUFP)                                                                  \
-    do {                                                                                        \
-        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);            \
-        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + C::TILE, wave_u);  \
+#define SA_FWD_ISSUE(KT, BUFP)                                                                          \
+    do {                                                                                                \
+        if constexpr (ADMA) {                                                                           \
+            dma_tile_asm(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);           \
+            dma_tile_asm(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + C::TILE, wave_u); \
+        } else {                                                                                        \
+            dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);               \
+            dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + C::TILE, wave_u);     \
+        }                                                                                               \
     } while (0)
 
     bf16x8 qf[C::NKS];
@@ -252,6 +259,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < C::NKS; ++ks)
             qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * h));
+        // consume Q here: hipcc then retires its loads before the loop instead of inside it, where its vmcnt would
+        // also wait for the asm LDS-DMA in flight
+#pragma unroll
+        for (int ks = 0; ks < C::NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
     }
     f32x16 o[C::NT];
 #pragma unroll
@@ -355,6 +366,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
     char* buf0 = smem;
     char* buf1 = smem + 2 * C::TILE;
     if (klo < khi) SA_FWD_ISSUE(klo, buf0);
+    if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // pairs of tiles (buffer 0 then 1) so every LDS address is register + immediate; odd tail peeled
     const int ntiles = khi > klo ? (khi - klo + C::KT - 1) / C::KT : 0;
@@ -362,9 +374,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
     for (int pr = 0; pr < ntiles / 2; ++pr, kt += 2 * C::KT) {
         SA_FWD_ISSUE(kt + C::KT, buf1);
         tile(buf0, kt);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (kt + 2 * C::KT < khi) SA_FWD_ISSUE(kt + 2 * C::KT, buf0);
         tile(buf1, kt + C::KT);
+        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     if (ntiles & 1) tile(buf0, kt);
@@ -397,31 +411,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
 // kernel's barrier per tile keeps the partners in lockstep: MFMA util 0.49 at VALU/MFMA 6.3).
 // K / V tiles by LDS-DMA: K_j and V_{j-1} are issued in phase 2j-2 and retired at the end of phase 2j-1 (two
 // buffers each; K_j is read in phases 2j (A) and 2j+1 (B), V_{j-1} in the same phases).
-// LDS-DMA of a [64][D] tile as inline asm: invisible to the compiler's waitcnt pass, which otherwise puts a
-// vmcnt(0) in front of the next LDS read of ANY buffer and so waits for the tile just issued; the caller retires
-// the pieces with its own s_waitcnt vmcnt before the barrier that publishes them.  m0 is saved / restored around
-// each piece (compiler-reserved), and the descriptor may be fresh from v_readfirstlane: s_nop 4 opens the string.
-template <int D, int W>
-__device__ __forceinline__ void dma_tile_asm(const DmaTile<D, W>& t, const void* base, int64_t tok, int rows, char* tile,
-                                             int wave_u) {
-    typedef int i32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t ad = reinterpret_cast<uint64_t>(base);
-    const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)ad),
-                      (int)(__builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32)) & 0xffff),
-                      (int)__builtin_amdgcn_readfirstlane((uint32_t)max(rows, 0) * (uint32_t)tok * 2u), kBufFlags};
-#pragma unroll
-    for (int i = 0; i < DmaTile<D, W>::NPW; ++i) {
-        const uint32_t lds = __builtin_amdgcn_readfirstlane(
-            (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)(tile + (wave_u + W * i) * 1024)));
-        int keep;
-        asm volatile(
-            "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lds), "v"(t.voff[i]), "s"(rs));
-    }
-}
-
 template <int D, bool F16>
 __global__ __launch_bounds__(512, 1) void fa_fwd_pp_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -476,6 +465,10 @@ __global__ __launch_bounds__(512, 1) void fa_fwd_pp_kernel(FwdArgs a) {
 #pragma unroll
         for (int ks = 0; ks < C::NKS; ++ks)
             qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * h));
+        // consume Q here: hipcc then retires its loads before the loop instead of inside it, where its vmcnt would
+        // also wait for the asm LDS-DMA in flight
+#pragma unroll
+        for (int ks = 0; ks < C::NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
     }
     f32x16 o[C::NT];
 #pragma unroll
@@ -662,9 +655,15 @@ static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
             const char* e = getenv("SCALING_AMD_FA_FWD_WAVES");  // 4 (default, measured faster) or 8
             return e && atoi(e) == 8 ? 8 : 4;
         }();
+        static const bool adma = [] {
+            const char* e = getenv("SCALING_AMD_FA_FWD_ADMA");
+            return e && atoi(e) == 1;
+        }();
         if (nw == 4) {
             dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128, 4>::BM - 1) / FwdV2<128, 4>::BM), block(256);
-            if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+            if (D == 128 && adma)
+                hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4, true>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+            else if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4>), grid, block, 4 * FwdV2<128>::TILE, st, a);
             else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, 4>), grid, block, 4 * FwdV2<64>::TILE, st, a);
             return;
         }
