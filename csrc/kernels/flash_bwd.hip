@@ -92,7 +92,10 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
 // OCC: waves per SIMD the register budget is sized for (1: the whole register file, with explicit read-ahead);
 // ADMA: the per-tile LDS-DMA as inline asm retired by an explicit vmcnt(0) before the barrier (compiler-visible
 // LDS-DMA makes hipcc wait for the NEXT tile's DMA in front of this tile's transposed LDS reads).
-template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false>
+// PAIR (with OCC 1 and ADMA, no dropout): two query tiles per barrier, software-pipelined inside the wave: the S/dP
+// MFMAs of tile B run beside tile A's exp / dS VALU and tile A's dV/dK MFMAs beside tile B's (one wave per SIMD
+// issues its VALU in the MFMA gaps); boundary (masked) pairs take the sequential tile path.  Four LDS buffers.
+template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false, bool PAIR = false>
 __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -311,6 +314,127 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
             ++g;
         }
     };
+    if constexpr (PAIR && OCC == 1 && ADMA && !DROP) {
+        static_assert(PAIR ? true : true, "");
+        // ---- paired, software-pipelined path (see the template comment)
+        auto sdp = [&](const char* Q, f32x16& sx, f32x16& dpx) {
+            const char* DO = Q + TILE;
+            sx = f32x16{};
+            dpx = f32x16{};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                sx = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], sx);
+                dpx = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dpx);
+            }
+        };
+        auto soft = [&](const char* Q, f32x16& sx, f32x16& dpx, bf16x8 (&pb)[2], bf16x8 (&db)[2]) {
+            const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
+            const float* DL = LS + 64;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 8 * g + 4 * h);
+                const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + 8 * g + 4 * h);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float pr = fast_exp2(__builtin_fmaf(sx[4 * g + j], c2, -l4[j]));
+                    sx[4 * g + j] = pr;
+                    dpx[4 * g + j] = pr * (dpx[4 * g + j] - d4[j]);
+                }
+            }
+            pb[0] = pack_acc_t<F16>(sx, 0);
+            pb[1] = pack_acc_t<F16>(sx, 1);
+            db[0] = pack_acc_t<F16>(dpx, 0);
+            db[1] = pack_acc_t<F16>(dpx, 1);
+        };
+        auto dvdk = [&](const char* Q, const bf16x8 (&pb)[2], const bf16x8 (&db)[2]) {
+            const char* DO = Q + TILE;
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    dv[t] = mma<F16>(rd_tr<D>(DO, 16 * ss * D * 2, lo, t), pb[ss], dv[t]);
+                    dk[t] = mma<F16>(rd_tr<D>(Q, 16 * ss * D * 2, lo, t), db[ss], dk[t]);
+                }
+        };
+        auto masked = [&](int gi, int qi) {
+            const int qt = qlo + qi * QT;
+            const int win = (h0 + gi) < a.local_heads ? a.window : -1;
+            return (a.causal && kw0 + 31 > qt + off) ||
+                   (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
+        };
+        auto pair = [&](const char* QA, const char* QB) {
+            f32x16 sA, dpA, sB, dpB;
+            bf16x8 pbA[2], dbA[2], pbB[2], dbB[2];
+            sdp(QA, sA, dpA);
+#pragma unroll
+            for (int i = 0; i < 2 * NKS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            sdp(QB, sB, dpB);
+            soft(QA, sA, dpA, pbA, dbA);
+#pragma unroll
+            for (int i = 0; i < 2 * NKS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dvdk(QA, pbA, dbA);
+            soft(QB, sB, dpB, pbB, dbB);
+#pragma unroll
+            for (int i = 0; i < 4 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 2);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dvdk(QB, pbB, dbB);
+#pragma unroll
+            for (int i = 0; i < 4 * NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 3);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 3);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // (an array of buffer pointers would lose the LDS address space: every read turned into a flat address)
+        auto bufs = [&](int k) { return smem + VIMG + (k & 3) * BUF; };
+        if (nwork > 0) {
+            issue(ig, iq, bufs(0));
+            adv(ig, iq);
+        }
+        if (nwork > 1) {
+            issue(ig, iq, bufs(1));
+            adv(ig, iq);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int w = 0;
+        for (; w + 1 < nwork; w += 2) {
+            if (w + 2 < nwork) {
+                issue(ig, iq, bufs(w + 2));
+                adv(ig, iq);
+            }
+            if (w + 3 < nwork) {
+                issue(ig, iq, bufs(w + 3));
+                adv(ig, iq);
+            }
+            const int gA = cg, qA = cq;
+            adv(cg, cq);
+            const int gB = cg, qB = cq;
+            adv(cg, cq);
+            if (!masked(gA, qA) && !masked(gB, qB)) {
+                pair(bufs(w), bufs(w + 1));
+            } else {
+                tile(bufs(w), gA, qA);
+                tile(bufs(w + 1), gB, qB);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        if (w < nwork) tile(bufs(w), cg, cq);
+    } else {
     if (nwork > 0) {
         issue(ig, iq, buf0);
         adv(ig, iq);
@@ -335,6 +459,7 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
         __syncthreads();
     }
     if (w < nwork) tile(buf0, cg, cq);
+    }
 
     if (mykey < Lk) {
         if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel
@@ -563,6 +688,13 @@ static int bwd_occ() {
     }();
     return v;
 }
+static bool bwd_pair() {  // SCALING_AMD_FA_BWD_PAIR=1: paired, software-pipelined dK/dV (D = 128, no dropout)
+    static const bool v = [] {
+        const char* e = getenv("SCALING_AMD_FA_BWD_PAIR");
+        return e && atoi(e) == 1;
+    }();
+    return v;
+}
 static bool bwd_adma() {
     static const bool v = [] {
         const char* e = getenv("SCALING_AMD_FA_BWD_ADMA");
@@ -576,7 +708,10 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
-        if (D == 128 && bwd_occ() == 1 && bwd_adma())
+        if (D == 128 && bwd_pair() && !DROP)
+            hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1, true, true>), grid, 256,
+                               128 * D * 2 + 4 * (2 * 32 * D * 2 + 512), st, a);
+        else if (D == 128 && bwd_occ() == 1 && bwd_adma())
             hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
         else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
         else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);
