@@ -60,7 +60,8 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--tp", type=int, default=1)
     p.add_argument("--pp", type=int, default=1)
     p.add_argument("--activation-checkpointing", type=str, default="disabled",
-                   choices=["disabled", "every_layer", "every_layer_keep_attention", "every_pipe_stage"])
+                   choices=["disabled", "every_layer", "every_layer_keep_attention", "every_layer_save_matmuls",
+                            "every_pipe_stage"])
     p.add_argument("--sequence-parallel", action="store_true")
     p.add_argument("--tp-comm-chunks", type=int, default=1,
                    help="row-parallel GEMM + TP all-reduce / SP reduce-scatter in this many overlapped token pieces")

@@ -49,6 +49,7 @@ from typing import Any, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ....ops.attention import stash_gemm
 from ....ops.gemm import linear as gemm_linear
 from ....ops.gemm import transpose2d, wgrad
 from ...utils.debug_env import side_streams_enabled
@@ -187,7 +188,7 @@ class _MultiLinear(torch.autograd.Function):
         b = None
         if has_bias:
             b = biases[0] if n == 1 else torch.cat(biases, dim=0)  # type: ignore[arg-type]
-        out = gemm_linear(x, w, b)
+        out = stash_gemm(lambda: gemm_linear(x, w, b))
         wt = _transposed(weights, w) if want_wt else None
         ctx.has_wt = wt is not None
         ctx.save_for_backward(x, wt if wt is not None else w, *weights)

@@ -16,11 +16,11 @@ from torch.utils.checkpoint import checkpoint
 from ....ops.attention import AttentionStash, attention_stash
 
 
-def _tracker_contexts(topology: Any, keep_attention: bool = False) -> tuple:
+def _tracker_contexts(topology: Any, keep_attention: bool = False, keep_gemms: bool = False) -> tuple:
     tracker = getattr(topology, "_model_parallel_constant_rng", None)
     saved: dict[str, Any] = {}
     # lives as long as this checkpoint's frame: recorded in the forward, drained by the recompute
-    stash = AttentionStash() if keep_attention else None
+    stash = AttentionStash(keep_gemms=keep_gemms) if (keep_attention or keep_gemms) else None
 
     @contextlib.contextmanager
     def forward_ctx() -> Iterator[None]:
@@ -46,15 +46,16 @@ def _tracker_contexts(topology: Any, keep_attention: bool = False) -> tuple:
 
 
 def checkpoint_with_rng(function: Callable[..., Any], topology: Any, preserve_rng_state: bool, *args: Any,
-                        keep_attention: bool = False) -> Any:
+                        keep_attention: bool = False, keep_gemms: bool = False) -> Any:
     """Non-reentrant checkpoint of ``function(*args)`` that replays the TP-constant RNG stream; with
-    ``keep_attention`` the flash-attention outputs of the first forward are kept and reused by the recompute."""
+    ``keep_attention`` the flash-attention outputs of the first forward are kept and reused by the recompute, with
+    ``keep_gemms`` also every linear layer's GEMM output (selective recompute of the element-wise work only)."""
     return checkpoint(
         function,
         *args,
         use_reentrant=False,
         preserve_rng_state=preserve_rng_state,
-        context_fn=lambda: _tracker_contexts(topology, keep_attention),
+        context_fn=lambda: _tracker_contexts(topology, keep_attention, keep_gemms),
     )
 
 

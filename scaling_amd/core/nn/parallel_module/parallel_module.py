@@ -217,12 +217,14 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         if self.training and ac == ActivationCheckpointingType.EVERY_PIPE_STAGE:
             return checkpoint_with_rng(self._forward_tuple_input, self.topology, True, *self._layers[0].input_to_tuple(x))
         if self.training and ac in (ActivationCheckpointingType.EVERY_LAYER,
-                                    ActivationCheckpointingType.EVERY_LAYER_KEEP_ATTENTION):
-            keep = ac == ActivationCheckpointingType.EVERY_LAYER_KEEP_ATTENTION
+                                    ActivationCheckpointingType.EVERY_LAYER_KEEP_ATTENTION,
+                                    ActivationCheckpointingType.EVERY_LAYER_SAVE_MATMULS):
+            gemms = ac == ActivationCheckpointingType.EVERY_LAYER_SAVE_MATMULS
+            keep = gemms or ac == ActivationCheckpointingType.EVERY_LAYER_KEEP_ATTENTION
             for layer in self._layers:
                 self._param_sync(layer)
                 x = checkpoint_with_rng(layer._forward_tuple_input, self.topology, True, *layer.input_to_tuple(x),
-                                        keep_attention=keep)
+                                        keep_attention=keep, keep_gemms=gemms)
             return x
         for layer in self._layers:
             self._param_sync(layer)

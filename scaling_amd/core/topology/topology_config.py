@@ -27,6 +27,10 @@ class ActivationCheckpointingType(Enum):
     # MI355X addition: per-layer recompute that keeps each layer's flash-attention output + LSE, so the backward's
     # recompute skips the attention forward (``ops.attention.AttentionStash``)
     EVERY_LAYER_KEEP_ATTENTION = "every_layer_keep_attention"
+    # MI355X addition: selective per-layer recompute -- the first forward also keeps every linear layer's GEMM output,
+    # so the recompute runs only the cheap element-wise work (norms, RoPE, SwiGLU, residual adds) and rebuilds the
+    # autograd graph around the kept outputs (``ops.attention.stash_gemm``)
+    EVERY_LAYER_SAVE_MATMULS = "every_layer_save_matmuls"
     DISABLED = "disabled"
 
 

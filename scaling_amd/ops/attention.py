@@ -17,7 +17,7 @@ from __future__ import annotations
 import contextlib
 import math
 import threading
-from typing import Any, Iterator, Optional
+from typing import Callable, Any, Iterator, Optional
 
 import torch
 
@@ -123,9 +123,13 @@ class AttentionStash:
     (everything else of the layer -- GEMMs, norms, RoPE -- is recomputed as usual).  Costs the attention output +
     LSE per layer in memory; saves one flash forward per layer and step."""
 
-    def __init__(self) -> None:
+    def __init__(self, keep_gemms: bool = False) -> None:
         self.items: list[Optional[tuple[torch.Tensor, torch.Tensor]]] = []
         self.pos = 0
+        # every_layer_save_matmuls: linear-layer GEMM outputs of the first forward (tensor, version at record time)
+        self.keep_gemms = keep_gemms
+        self.gemms: list[Optional[tuple[torch.Tensor, int]]] = []
+        self.gpos = 0
 
 
 _stash_state = threading.local()
@@ -141,6 +145,29 @@ def attention_stash(stash: Optional[AttentionStash], mode: str) -> Iterator[None
         yield
     finally:
         _stash_state.cur = prev
+
+
+def stash_gemm(compute: Callable[[], torch.Tensor]) -> torch.Tensor:
+    """A linear layer's GEMM output through the checkpoint stash (``every_layer_save_matmuls``): the region's first
+    forward records ``compute()``'s output, the recompute in the backward returns it instead of running the GEMM again
+    (falling back to ``compute()`` when the kept tensor was modified in place since, e.g. a LoRA up-projection
+    accumulated into it).  Outside such a region this is just ``compute()``."""
+    cur = getattr(_stash_state, "cur", None)
+    if cur is None or not cur[0].keep_gemms:
+        return compute()
+    stash, mode = cur
+    if mode == "replay":
+        if stash.gpos < len(stash.gemms):
+            item = stash.gemms[stash.gpos]
+            stash.gemms[stash.gpos] = None  # the rebuilt graph's saved tensors hold it from here on
+            stash.gpos += 1
+            if item is not None and item[0]._version == item[1]:
+                return item[0]
+        return compute()
+    out = compute()
+    kept = out.detach()
+    stash.gemms.append((kept, kept._version))
+    return out
 
 
 def _fa_fwd_stashed(q, k, v, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k):

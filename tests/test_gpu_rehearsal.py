@@ -213,15 +213,17 @@ def test_keep_attention_checkpointing_gpu(tmp_path):
 
     _make_data(tmp_path / "data")
     losses = {}
-    for ac in ("disabled", "every_layer", "every_layer_keep_attention"):
+    for ac in ("disabled", "every_layer", "every_layer_keep_attention", "every_layer_save_matmuls"):
         cfg = _config(tmp_path, 1, 1, 1, precision="bfloat16", masked_softmax={"kernel": "flash_attention"},
                       hidden_size=128, sequence_length=128, checkpointing=ac)
         cfg["trainer"]["save_dir"] = None
         cfg["trainer"]["load_dir"] = None
         losses[ac] = [m["training/loss"] for m in _train(tmp_path, cfg, 1, ac)]
-    # keep-attention reproduces plain per-layer checkpointing bit for bit; against no checkpointing the recompute
-    # re-associates some gradient sums (autograd accumulation order at the checkpoint seams), so only rounding-close
+    # keep-attention (and the selective recompute that also keeps the GEMM outputs) reproduces plain per-layer
+    # checkpointing bit for bit; against no checkpointing the recompute re-associates some gradient sums (autograd
+    # accumulation order at the checkpoint seams), so only rounding-close
     assert losses["every_layer_keep_attention"] == losses["every_layer"], losses
+    assert losses["every_layer_save_matmuls"] == losses["every_layer"], losses
     assert losses["every_layer"][0] == losses["disabled"][0]
     assert all(abs(a - b) <= 2e-3 * abs(b) for a, b in zip(losses["every_layer"], losses["disabled"])), losses
 

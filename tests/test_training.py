@@ -185,9 +185,75 @@ def test_keep_attention_checkpointing_matches_every_layer(tmp_path, mp, pp, worl
     attention has no flash kernel to keep, so this pins the mode's plumbing; the GPU test pins the reuse)."""
     _make_data(tmp_path / "data")
     runs = {}
-    for ac in ("every_layer", "every_layer_keep_attention"):
+    for ac in ("every_layer", "every_layer_keep_attention", "every_layer_save_matmuls"):
         cfg = _config(tmp_path, mp, pp, world, checkpointing=ac)
         cfg["trainer"]["save_dir"] = None
         cfg["trainer"]["load_dir"] = None
         runs[ac] = [m["training/loss"] for m in _run(tmp_path, cfg, world, ac)]
     assert runs["every_layer"] == runs["every_layer_keep_attention"]
+    # selective recompute (GEMM outputs kept, element-wise work recomputed) is the same arithmetic
+    assert runs["every_layer"] == runs["every_layer_save_matmuls"]
+
+
+def test_save_matmuls_checkpointing_skips_gemms_in_recompute():
+    """``every_layer_save_matmuls``: the backward's recompute of a checkpointed layer runs no linear-layer GEMM (every
+    forward GEMM output is replayed from the first forward), gradients equal plain per-layer checkpointing, and a kept
+    output modified in place after the first forward is recomputed instead of replayed."""
+    import torch
+
+    import scaling_amd.core.nn.linear.main_grad as mg
+    from scaling_amd.core.nn.parallel_module.activation_checkpointing import checkpoint_with_rng
+    from scaling_amd.models import llama_architecture
+    from scaling_amd.ops.attention import AttentionStash, attention_stash, stash_gemm
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+    from scaling_amd.transformer.model.layers import TransformerLayer
+    from scaling_amd.transformer.model.layers.base import TransformerLayerIO
+
+    torch.manual_seed(0)
+    arch = TransformerArchitectureConfig(**llama_architecture("llama_tiny", sequence_length=32, vocab_size=64))
+    layer = TransformerLayer(arch, layer_index=0)
+    real = mg.gemm_linear
+    calls = []
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    grads = {}
+    for gemms in (False, True):
+        calls.clear()
+        layer.zero_grad(set_to_none=True)
+        dt = next(layer.parameters()).dtype
+        x = torch.randn(2, 32, arch.hidden_size, generator=torch.Generator().manual_seed(1)).to(dt).requires_grad_()
+        cu = torch.tensor([0, 32, 64], dtype=torch.int32)
+        pos = torch.arange(32).unsqueeze(0).expand(2, -1).contiguous()
+        io = TransformerLayerIO(activations=x, position_ids=pos, cumulative_seq_lengths_padded=cu,
+                                cumulative_seq_lengths=cu)
+        mg.gemm_linear = counting
+        try:
+            out = checkpoint_with_rng(layer._forward_tuple_input, None, True, *layer.input_to_tuple(io),
+                                      keep_gemms=gemms)
+            n_fwd = len(calls)
+            out.activations.pow(2).mean().backward()
+        finally:
+            mg.gemm_linear = real
+        assert n_fwd > 0
+        assert len(calls) == (n_fwd if gemms else 2 * n_fwd), (gemms, n_fwd, len(calls))
+        grads[gemms] = [x.grad.clone()] + [p.grad.clone() for p in layer.parameters() if p.grad is not None]
+    for a, b in zip(grads[False], grads[True]):
+        assert torch.equal(a, b)
+
+    # a kept output changed in place (a LoRA up-projection accumulating into it) is recomputed, not replayed
+    stash = AttentionStash(keep_gemms=True)
+    with attention_stash(stash, "record"):
+        y = stash_gemm(lambda: torch.ones(3))
+    y.add_(1)
+    with attention_stash(stash, "replay"):
+        z = stash_gemm(lambda: torch.full((3,), 7.0))
+    assert torch.equal(z, torch.full((3,), 7.0))
+    stash = AttentionStash(keep_gemms=True)
+    with attention_stash(stash, "record"):
+        y = stash_gemm(lambda: torch.ones(3))
+    with attention_stash(stash, "replay"):
+        z = stash_gemm(lambda: torch.full((3,), 7.0))
+    assert torch.equal(z, torch.ones(3))
