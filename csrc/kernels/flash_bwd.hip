@@ -503,7 +503,8 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: workgroup = 4 waves x 32 queries of one (segment, q head); query on the lane (Q, dO rows are
 // register-resident B operands), K / V tiles of 64 keys double-buffered in LDS by LDS-DMA.  Per 32-key block:
 //   S^T = K Q^T, dP^T = V dO^T, p = exp2(S c - lse2), dS = p (dP - delta), dQ^T += K^T dS^T.
-template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false>
+// RA: explicit LDS read-ahead pinned by sched barriers (hipcc sinks each read right in front of its MFMA)
+template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false, bool RA = false>
 __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -579,10 +580,31 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             f32x16 s = f32x16{}, dp = f32x16{};
+            if constexpr (RA) {
+                constexpr int PD = 2;
+                bf16x8 rk[PD], rv[PD];
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row(ks)), qf[ks], s);
-                dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row(ks)), df[ks], dp);
+                for (int ks = 0; ks < PD; ++ks) {
+                    rk[ks] = rd_row<D>(K, 32 * b * D * 2, lo.row(ks));
+                    rv[ks] = rd_row<D>(V, 32 * b * D * 2, lo.row(ks));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    s = mma<F16>(rk[ks % PD], qf[ks], s);
+                    dp = mma<F16>(rv[ks % PD], df[ks], dp);
+                    if (ks + PD < NKS) {
+                        rk[ks % PD] = rd_row<D>(K, 32 * b * D * 2, lo.row(ks + PD));
+                        rv[ks % PD] = rd_row<D>(V, 32 * b * D * 2, lo.row(ks + PD));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row(ks)), qf[ks], s);
+                    dp = mma<F16>(rd_row<D>(V, 32 * b * D * 2, lo.row(ks)), df[ks], dp);
+                }
             }
             // key of register j: kt + 32b + 4h + crow(j)
 #pragma unroll
@@ -607,12 +629,30 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
                     dp[r] = p * (dp[r] - dlt);
                 }
             }
+            if constexpr (RA) {
+                const bf16x8 dbs[2] = {pack_acc_t<F16>(dp, 0), pack_acc_t<F16>(dp, 1)};
+                constexpr int NS = 2 * NT, PD = 2;  // step i = (ss = i / NT, t = i % NT)
+                bf16x8 fk[PD];
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                const bf16x8 db = pack_acc_t<F16>(dp, ss);
-                const int kb = (32 * b + 16 * ss) * D * 2;
+                for (int i = 0; i < PD; ++i) fk[i] = rd_tr<D>(K, (32 * b + 16 * (i / NT)) * D * 2, lo, i % NT);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int t = 0; t < NT; ++t) dq[t] = mma<F16>(rd_tr<D>(K, kb, lo, t), db, dq[t]);
+                for (int i = 0; i < NS; ++i) {
+                    dq[i % NT] = mma<F16>(fk[i % PD], dbs[i / NT], dq[i % NT]);
+                    if (i + PD < NS) {
+                        const int j = i + PD;
+                        fk[i % PD] = rd_tr<D>(K, (32 * b + 16 * (j / NT)) * D * 2, lo, j % NT);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else {
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const bf16x8 db = pack_acc_t<F16>(dp, ss);
+                    const int kb = (32 * b + 16 * ss) * D * 2;
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) dq[t] = mma<F16>(rd_tr<D>(K, kb, lo, t), db, dq[t]);
+                }
             }
         }
     };
@@ -722,7 +762,12 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
     {
         dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
-        if (D == 128 && bwd_occ() == 1 && bwd_adma())
+        static const bool ra = [] {
+            const char* e = getenv("SCALING_AMD_FA_BWD_RA");
+            return e && atoi(e) == 1;
+        }();
+        if (D == 128 && ra) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 2, false, true>), grid, 256, lds, st, a);
+        else if (D == 128 && bwd_occ() == 1 && bwd_adma())
             hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
         else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
         else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);

@@ -193,7 +193,9 @@ struct FwdV2 {
 // drift apart, so one workgroup's softmax can overlap the other's MFMAs on a SIMD)
 // ADMA: the per-tile LDS-DMA as inline asm retired by an explicit vmcnt(0) before the barrier (with compiler-visible
 // LDS-DMA hipcc waits for the NEXT tile's DMA in front of this tile's transposed V reads)
-template <int D, bool F16, bool DROP, int NW = 8, bool ADMA = false>
+// RA: explicit LDS read-ahead (K fragments RA_K MFMAs ahead in S = K Q^T, V^T fragments RA_V ahead in O += V^T P^T),
+// pinned by sched barriers: hipcc otherwise sinks every read right in front of the MFMA that consumes it
+template <int D, bool F16, bool DROP, int NW = 8, bool ADMA = false, bool RA = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     using C = FwdV2<D, NW>;
@@ -275,16 +277,33 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
     auto tile = [&](const char* K, int kt) {
         const char* V = K + C::TILE;
         f32x16 s[2] = {f32x16{}, f32x16{}};
+        if constexpr (RA) {
+            constexpr int NF = 2 * C::NKS, PK = 4;  // fragment f = (ks = f / 2, b = f % 2)
+            bf16x8 kb[PK];
 #pragma unroll
-        for (int ks = 0; ks < C::NKS; ++ks)
+            for (int f = 0; f < PK; ++f) kb[f] = *reinterpret_cast<const bf16x8*>(K + 32 * (f & 1) * D * 2 + rowoff[f >> 1]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-                s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
-        // keep the K fragment reads one or two MFMAs ahead instead of hoisting all of them
+            for (int f = 0; f < NF; ++f) {
+                s[f & 1] = mma<F16>(kb[f % PK], qf[f >> 1], s[f & 1]);
+                if (f + PK < NF) {
+                    const int g = f + PK;
+                    kb[f % PK] = *reinterpret_cast<const bf16x8*>(K + 32 * (g & 1) * D * 2 + rowoff[g >> 1]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < 2 * C::NKS; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            for (int ks = 0; ks < C::NKS; ++ks)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
+            // keep the K fragment reads one or two MFMAs ahead instead of hoisting all of them
+#pragma unroll
+            for (int i = 0; i < 2 * C::NKS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            }
         }
         // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
         const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
@@ -345,21 +364,44 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void fa_fwd_v2_kernel(FwdArgs a) {
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
+        if constexpr (RA) {
+            // step i = (t, b, ss) in the original order; V^T fragments PV steps ahead
+            constexpr int NS = 4 * C::NT, PV = 3;
+            auto vfrag = [&](int i) -> bf16x8 {
+                const int t = i / 4, b = (i / 2) & 1, ss = i & 1;
+                const int kb = (32 * b + 16 * ss) * D * 2;
+                const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
+                const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
+                return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+            };
+            bf16x8 vb[PV];
 #pragma unroll
-        for (int t = 0; t < C::NT; ++t)
+            for (int i = 0; i < PV; ++i) vb[i] = vfrag(i);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
+            for (int i = 0; i < NS; ++i) {
+                const int t = i / 4, b = (i / 2) & 1, ss = i & 1;
+                o[t] = mma<F16>(vb[i % PV], pf[b][ss], o[t]);
+                if (i + PV < NS) vb[i % PV] = vfrag(i + PV);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
 #pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    const int kb = (32 * b + 16 * ss) * D * 2;
-                    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
-                    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
-                    o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
-                }
+            for (int t = 0; t < C::NT; ++t)
 #pragma unroll
-        for (int i = 0; i < 4 * C::NT; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) {
+                        const int kb = (32 * b + 16 * ss) * D * 2;
+                        const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
+                        const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
+                        o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
+                    }
+#pragma unroll
+            for (int i = 0; i < 4 * C::NT; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+            }
         }
     };
 
@@ -661,7 +703,13 @@ static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
         }();
         if (nw == 4) {
             dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128, 4>::BM - 1) / FwdV2<128, 4>::BM), block(256);
-            if (D == 128 && adma)
+            static const bool ra = [] {
+                const char* e = getenv("SCALING_AMD_FA_FWD_RA");
+                return e && atoi(e) == 1;
+            }();
+            if (D == 128 && ra)
+                hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4, false, true>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+            else if (D == 128 && adma)
                 hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4, true>), grid, block, 4 * FwdV2<128>::TILE, st, a);
             else if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 4>), grid, block, 4 * FwdV2<128>::TILE, st, a);
             else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, 4>), grid, block, 4 * FwdV2<64>::TILE, st, a);
