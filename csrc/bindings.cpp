@@ -382,6 +382,36 @@ at::Tensor gemv_swiglu(const at::Tensor& x, const at::Tensor& W) {
                     (int)K, cur_stream(), 2, nullptr, 0);
     return y;
 }
+// ... with the RMSNorm in front fused into the same pass: s = x (+ add); y = gemv(rms_norm(s, gamma, eps), W) with
+// epi 0 (plain) or 2 (SwiGLU over [gate; up]), the normalised row kept in fp32; returns (s, y), s written by the
+// kernel when add is given
+bool gemv_norm_ok(const at::Tensor& x, const at::Tensor& W, const at::Tensor& gamma) {
+    if (!gemv_ok(x, W) || !x.is_contiguous()) return false;
+    if (!(gamma.is_cuda() && gamma.dim() == 1 && gamma.numel() == x.size(1) && gamma.is_contiguous() &&
+          gamma.scalar_type() == x.scalar_type() && (uintptr_t)gamma.data_ptr() % 16 == 0))
+        return false;
+    return true;
+}
+std::vector<at::Tensor> gemv_norm(const at::Tensor& x, c10::optional<at::Tensor> add, const at::Tensor& gamma,
+                                  double eps, const at::Tensor& W, int64_t epi) {
+    TORCH_CHECK(gemv_norm_ok(x, W, gamma) && (epi == 0 || (epi == 2 && W.size(0) % 2 == 0)),
+                "gemv_norm: unsupported operands");
+    const int64_t M = x.size(0), K = W.size(1), N = epi == 2 ? W.size(0) / 2 : W.size(0);
+    const at::DeviceGuard g(x.device());
+    at::Tensor s = x;
+    const void* ap = nullptr;
+    if (add.has_value() && add->defined()) {
+        TORCH_CHECK(add->sizes() == x.sizes() && add->is_contiguous() && add->scalar_type() == x.scalar_type() &&
+                        (uintptr_t)add->data_ptr() % 16 == 0, "gemv_norm: add must be a contiguous, aligned [M, K]");
+        s = at::empty_like(x);
+        ap = add->data_ptr();
+    }
+    auto y = at::empty({M, N}, x.options());
+    sa_launch::gemv(dt(x), (int)M, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), nullptr, y.data_ptr(), N, (int)N,
+                    (int)K, cur_stream(), (int)epi, nullptr, 0, gamma.data_ptr(), ap, ap ? s.data_ptr() : nullptr,
+                    (float)eps);
+    return {s, y};
+}
 
 // ------------------------------------------------------------------ GEMM (weight gradient)
 // C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
@@ -667,6 +697,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemv", &gemv, "y = x W^T (+ b) for at most 4 rows of x (decode-time linear layers)", py::arg("x"), py::arg("W"), py::arg("bias") = py::none());
     m.def("gemv_residual", &gemv_residual, "y = x W^T + res for at most 4 rows (decode MLP-out + residual)");
     m.def("gemv_swiglu", &gemv_swiglu, "y = silu(x Wg^T) * (x Wu^T) for W = [Wg; Wu], at most 4 rows (decode)");
+    m.def("gemv_norm_ok", &gemv_norm_ok, "whether gemv_norm supports these operands");
+    m.def("gemv_norm", &gemv_norm, "(s, gemv(rms_norm(s), W)) with s = x (+ add); epi 0 plain, 2 SwiGLU (decode)",
+          py::arg("x"), py::arg("add"), py::arg("gamma"), py::arg("eps"), py::arg("W"), py::arg("epi") = 0);
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");
     m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for k-major bf16 operands (weight-gradient GEMM)");
     m.def("rope", &rope, "rotary embedding (fwd / inverse), optional strided / in-place output", py::arg("x"), py::arg("cos"), py::arg("sin"), py::arg("pos"), py::arg("rot_dim"), py::arg("seq_len"), py::arg("interleaved"), py::arg("inverse"), py::arg("out") = py::none());

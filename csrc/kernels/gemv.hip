@@ -13,8 +13,17 @@
 //  * SWIGLU: W holds [gate; up] (2F rows); the wave streams rows n and F + n and writes
 //    y[:, n] = rnd(rnd(silu(g)) * u) with g, u rounded as the unfused GEMV stores them -- bit-identical to
 //    gemv + swiglu_fwd_kernel.
+// Decode prologue (NORM): the RMSNorm in front of the projection (optionally after the residual add
+// s = rnd(x + add)) runs inside the same single pass over the weights.  Every wave already reads all of x, so it
+// also accumulates sum(s^2) and dots the weights with s * gamma; the row's rstd scales the dot product at the end:
+//     y = rstd * sum_k w_k s_k gamma_k      (fp32; the unfused path rounds s * rstd and * gamma to bf16 first)
+// No prologue pass, no barrier, no extra launch: the two latency-bound norm launches per layer and token go away.
+// The wave that owns output row 0 also writes s (the new residual stream).  Eager and graph decoding both run this
+// kernel, so their tokens stay identical; against norm + GEMV it differs by the two skipped bf16 roundings.
 #include "common.h"
 #include "launch.h"
+
+#include <cstdlib>
 
 using namespace sa;
 
@@ -22,52 +31,77 @@ namespace {
 
 enum { EPI_NONE = 0, EPI_RES = 1, EPI_SWIGLU = 2 };
 
-template <int M, int NR, typename E>
+template <typename E>
+struct NormArgs {
+    const E* g;      // RMSNorm weight [K]; nullptr: no norm
+    const E* add;    // residual added before the norm ([M, K] contiguous) or nullptr
+    E* sum;          // rnd(x + add), written by the wave of output row 0 when add != nullptr
+    float eps;
+};
+
+template <int M, int NR, typename E, bool NORM>
 __device__ __forceinline__ void gemv_rows(const E* __restrict__ x, int64_t ldx, const E* const (&w)[NR], int K,
-                                          int lane, float (&acc)[NR][M]) {
+                                          int lane, float (&acc)[NR][M], const NormArgs<E>& na, bool write_sum) {
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-    constexpr int U = 4 / NR;
-    const int G = K >> 3;  // 8-element pieces per row
-    int g = lane;
-    for (; g + 64 * (U - 1) < G; g += 64 * U) {
-        float wv[NR][U][8];
+    float ss[M];
 #pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int u = 0; u < U; ++u) V8<E>::ld(w[r] + 8 * (g + 64 * u), wv[r][u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-                float xv[8];
-                V8<E>::ld(x + m * ldx + 8 * (g + 64 * u), xv);
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) acc[r][m] = __builtin_fmaf(wv[r][u][i], xv[i], acc[r][m]);
-            }
-    }
-    for (; g < G; g += 64) {
-        float wv[NR][8];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) V8<E>::ld(w[r] + 8 * g, wv[r]);
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+    // one 8-element piece p of every input row against the weight pieces wv (NR rows)
+    auto piece = [&](int p, const float (&wv)[NR][8]) {
+        float gv[8];
+        if constexpr (NORM) V8<E>::ld(na.g + 8 * p, gv);
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             float xv[8];
-            V8<E>::ld(x + m * ldx + 8 * g, xv);
+            V8<E>::ld(x + m * ldx + 8 * p, xv);
+            if constexpr (NORM) {
+                if (na.add != nullptr) {
+                    float av[8];
+                    V8<E>::ld(na.add + (int64_t)m * K + 8 * p, av);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) xv[i] = rnd<E>(xv[i] + av[i]);
+                    if (write_sum) V8<E>::st(na.sum + (int64_t)m * K + 8 * p, xv);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    ss[m] = __builtin_fmaf(xv[i], xv[i], ss[m]);
+                    xv[i] *= gv[i];
+                }
+            }
 #pragma unroll
             for (int r = 0; r < NR; ++r)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) acc[r][m] = __builtin_fmaf(wv[r][i], xv[i], acc[r][m]);
         }
+    };
+    constexpr int U = 4 / NR;
+    const int G = K >> 3;  // 8-element pieces per row
+    int g = lane;
+    for (; g + 64 * (U - 1) < G; g += 64 * U) {
+        float wv[U][NR][8];
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) V8<E>::ld(w[r] + 8 * (g + 64 * u), wv[u][r]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) piece(g + 64 * u, wv[u]);
+    }
+    for (; g < G; g += 64) {
+        float wv[NR][8];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) V8<E>::ld(w[r] + 8 * g, wv[r]);
+        piece(g, wv);
     }
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
+    for (int m = 0; m < M; ++m) {
+        float rstd = 1.f;
+        if constexpr (NORM) rstd = rsqrtf(wave_sum(ss[m]) / K + na.eps);
 #pragma unroll
-        for (int m = 0; m < M; ++m) acc[r][m] = wave_sum(acc[r][m]);
+        for (int r = 0; r < NR; ++r) acc[r][m] = wave_sum(acc[r][m]) * rstd;
+    }
 }
 
 // lane m < M picks input m's value out of the per-input accumulators (all lanes hold every sum after wave_sum)
@@ -80,61 +114,102 @@ __device__ __forceinline__ float pick(const float (&a)[M], int lane) {
     return v;
 }
 
-template <int M, int EPI, typename E>
+// RPW output rows per wave (consecutive rows r, r + 1): the NORM kernels take 2, which halves the per-weight-byte
+// work on x / add / gamma (every wave recomputes the normalised row for the pieces it streams)
+template <int M, int EPI, typename E, bool NORM, int RPW>
 __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int64_t ldx, const E* __restrict__ W,
                                                    int64_t ldw, const E* __restrict__ bias, const E* __restrict__ res,
-                                                   int64_t ldr, E* __restrict__ y, int64_t ldy, int N, int K) {
+                                                   int64_t ldr, E* __restrict__ y, int64_t ldy, int N, int K,
+                                                   NormArgs<E> na) {
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= N) return;  // wave-uniform
-    constexpr int NR = EPI == EPI_SWIGLU ? 2 : 1;
+    const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    if (row >= N) return;  // wave-uniform (N % RPW == 0)
+    constexpr int NS = EPI == EPI_SWIGLU ? 2 : 1;  // weight rows per output row
+    constexpr int NR = NS * RPW;
     const E* w[NR];
-    w[0] = W + (int64_t)row * ldw;
-    if constexpr (NR == 2) w[NR - 1] = W + (int64_t)(row + N) * ldw;  // up row F + n
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        w[q] = W + (int64_t)(row + q) * ldw;
+        if constexpr (NS == 2) w[RPW + q] = W + (int64_t)(row + q + N) * ldw;  // up row F + n
+    }
     float acc[NR][M];
-    gemv_rows<M, NR, E>(x, ldx, w, K, lane, acc);
+    gemv_rows<M, NR, E, NORM>(x, ldx, w, K, lane, acc, na, NORM && row == 0);
     if (lane < M) {
-        float v = pick<M>(acc[0], lane);
-        if constexpr (EPI == EPI_SWIGLU) {
-            const float a = rnd<E>(v), b = rnd<E>(pick<M>(acc[NR - 1], lane));
-            v = rnd<E>(a / (1.f + __expf(-a))) * b;
-        } else {
-            if (bias != nullptr) v += IO<E>::ld(bias, row);
-            if constexpr (EPI == EPI_RES) v = rnd<E>(v) + IO<E>::ld(res, (int64_t)lane * ldr + row);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            float v = pick<M>(acc[q], lane);
+            if constexpr (EPI == EPI_SWIGLU) {
+                const float a = rnd<E>(v), b = rnd<E>(pick<M>(acc[RPW + q], lane));
+                v = rnd<E>(a / (1.f + __expf(-a))) * b;
+            } else {
+                if (bias != nullptr) v += IO<E>::ld(bias, row + q);
+                if constexpr (EPI == EPI_RES) v = rnd<E>(v) + IO<E>::ld(res, (int64_t)lane * ldr + row + q);
+            }
+            IO<E>::st(y, (int64_t)lane * ldy + row + q, v);
         }
-        IO<E>::st(y, (int64_t)lane * ldy + row, v);
     }
 }
 
-template <int EPI, typename E>
-void launch(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
-            void* y, int64_t ldy, int N, int K, hipStream_t st) {
-    const dim3 grid((unsigned)((N + 3) / 4)), block(256);
+int rows_per_wave(bool norm, int N) {
+    static const int env = [] {
+        const char* e = std::getenv("SCALING_AMD_GEMV_RPW");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int r = env > 0 ? env : (norm ? 2 : 1);
+    return (r == 2 && N % 2 == 0) ? 2 : 1;
+}
+
+template <int EPI, typename E, bool NORM, int RPW>
+void launch_r(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
+              void* y, int64_t ldy, int N, int K, hipStream_t st, NormArgs<E> na) {
+    const dim3 grid((unsigned)((N + 4 * RPW - 1) / (4 * RPW))), block(256);
     const E *xp = (const E*)x, *wp = (const E*)W, *bp = (const E*)b, *rp = (const E*)r;
     E* yp = (E*)y;
     switch (M) {
-        case 1: hipLaunchKernelGGL((gemv_kernel<1, EPI, E>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K); break;
-        case 2: hipLaunchKernelGGL((gemv_kernel<2, EPI, E>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K); break;
-        case 3: hipLaunchKernelGGL((gemv_kernel<3, EPI, E>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K); break;
-        default: hipLaunchKernelGGL((gemv_kernel<4, EPI, E>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K); break;
+        case 1: hipLaunchKernelGGL((gemv_kernel<1, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        case 2: hipLaunchKernelGGL((gemv_kernel<2, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        case 3: hipLaunchKernelGGL((gemv_kernel<3, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        default: hipLaunchKernelGGL((gemv_kernel<4, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
     }
+}
+
+template <int EPI, typename E, bool NORM>
+void launch(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
+            void* y, int64_t ldy, int N, int K, hipStream_t st, NormArgs<E> na) {
+    if (rows_per_wave(NORM, N) == 2) launch_r<EPI, E, NORM, 2>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else launch_r<EPI, E, NORM, 1>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+}
+
+template <int EPI, typename E>
+void launch_n(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
+              void* y, int64_t ldy, int N, int K, hipStream_t st, const NormArgs<E>& na) {
+    if (na.g != nullptr) launch<EPI, E, true>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else launch<EPI, E, false>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
 }
 
 template <typename E>
 void launch_epi(int epi, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r,
-                int64_t ldr, void* y, int64_t ldy, int N, int K, hipStream_t st) {
-    if (epi == EPI_SWIGLU) launch<EPI_SWIGLU, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st);
-    else if (epi == EPI_RES) launch<EPI_RES, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st);
-    else launch<EPI_NONE, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st);
+                int64_t ldr, void* y, int64_t ldy, int N, int K, hipStream_t st, const NormArgs<E>& na) {
+    if (epi == EPI_SWIGLU) launch_n<EPI_SWIGLU, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else if (epi == EPI_RES) launch_n<EPI_RES, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else launch_n<EPI_NONE, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
 }
 
 }  // namespace
 
 namespace sa_launch {
-// epi 0: y = x W^T (+ b); 1: y = rnd(x W^T (+ b)) + res; 2: SwiGLU over W = [gate; up] (N = F output columns)
+// epi 0: y = x W^T (+ b); 1: y = rnd(x W^T (+ b)) + res; 2: SwiGLU over W = [gate; up] (N = F output columns).
+// norm_w != nullptr: x is first replaced by rms_norm(x (+ norm_add), norm_w, eps) inside the same pass
+// (norm_add / norm_sum [M, K] contiguous; norm_sum receives x + norm_add).
 void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, void* y, int64_t ldy,
-          int N, int K, hipStream_t st, int epi, const void* res, int64_t ldr) {
-    if (dtype == DT_F16) launch_epi<_Float16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st);
-    else launch_epi<u16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st);
+          int N, int K, hipStream_t st, int epi, const void* res, int64_t ldr, const void* norm_w, const void* norm_add,
+          void* norm_sum, float eps) {
+    if (dtype == DT_F16) {
+        const NormArgs<_Float16> na{(const _Float16*)norm_w, (const _Float16*)norm_add, (_Float16*)norm_sum, eps};
+        launch_epi<_Float16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
+    } else {
+        const NormArgs<u16> na{(const u16*)norm_w, (const u16*)norm_add, (u16*)norm_sum, eps};
+        launch_epi<u16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
+    }
 }
 }  // namespace sa_launch

@@ -147,5 +147,6 @@ void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64
 namespace sa_launch {
 // gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ b) for M <= 4 (decode-time linear layers), bf16 / fp16, K % 8 == 0
 void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, void* y, int64_t ldy,
-          int N, int K, hipStream_t st, int epi = 0, const void* res = nullptr, int64_t ldr = 0);
+          int N, int K, hipStream_t st, int epi = 0, const void* res = nullptr, int64_t ldr = 0,
+          const void* norm_w = nullptr, const void* norm_add = nullptr, void* norm_sum = nullptr, float eps = 0.f);
 }  // namespace sa_launch

@@ -27,7 +27,7 @@ from ...topology import Topology
 from ..linear import ColumnParallelLinear, RowParallelLinear
 from ..linear.fused import fused_column_linear
 from ..linear.utils import all_concat, all_reduce_scatter_to_sequence_parallel, all_shard
-from ..linear.main_grad import invalidate_transposed_weights
+from ..linear.main_grad import adjacent_weights, invalidate_transposed_weights
 from ..lora import ParallelLoRa
 from ..lora_config import LoRaConfig, LoRAModuleType
 from ..masked_softmax import MaskedSoftmax, MaskedSoftmaxConfig, MaskedSoftmaxKernel
@@ -377,13 +377,45 @@ class ParallelSelfAttention(torch.nn.Module):
         b, s, _ = x.shape
         T = b * s
         hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
-        if self.qkv_in_one:
-            base = self.query_key_value(x)
-            qkv = base.view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
-            return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :], base
-        base = fused_column_linear(x, [self.query, self.key, self.value], self.topology)
-        q, k, v = self._views(base, T)
+        base = self.query_key_value(x) if self.qkv_in_one else fused_column_linear(
+            x, [self.query, self.key, self.value], self.topology)
+        q, k, v = self._split_base(base, T)
         return q, k, v, base
+
+    def _split_base(self, base: torch.Tensor, T: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        if self.qkv_in_one:
+            hd, nq = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition
+            qkv = base.view(T, nq, 3 * hd)  # per-head interleaved [q|k|v]
+            return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :]
+        return self._views(base, T)
+
+    def decode_norm_project(self, x: torch.Tensor, norm: torch.nn.Module) -> Optional[torch.Tensor]:
+        """The q/k/v projection of ``norm(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, bias-free,
+        no pending LoRA) as ONE GEMV launch that folds the RMSNorm into its pass over the weights
+        (``ext().gemv_norm``; the normalised row stays fp32); pass the result to ``forward(..., projected_base=...)``.  None when the fused
+        path does not apply (the caller runs the norm and the plain forward)."""
+        prologue = getattr(norm, "gemv_prologue", None)
+        nw = prologue() if prologue is not None and _DECODE_FUSED else None
+        if nw is None or x.dim() != 3 or not use_native(x) or not x.is_contiguous():
+            return None
+        K = x.shape[-1]
+        rows = x.numel() // K if K else 0
+        if not 0 < rows <= 4:
+            return None
+        if self.lora_config is not None and not self.lora_merged_state:
+            return None
+        mods = [self.query_key_value] if self.qkv_in_one else [self.query, self.key, self.value]
+        weights = [m.weight for m in mods]
+        if torch.is_grad_enabled() and (x.requires_grad or nw[0].requires_grad or any(w.requires_grad for w in weights)):
+            return None
+        if any(getattr(m, "bias_param", None) is not None for m in mods):
+            return None
+        w = weights[0] if len(weights) == 1 else adjacent_weights(weights)
+        x2 = x.reshape(rows, K)
+        if w is None or not ext().gemv_norm_ok(x2, w, nw[0]):
+            return None
+        _, base = ext().gemv_norm(x2, None, nw[0], nw[1], w, 0)
+        return base.view(*x.shape[:-1], w.shape[0])
 
     def _views(self, base: torch.Tensor, T: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
@@ -478,7 +510,7 @@ class ParallelSelfAttention(torch.nn.Module):
                 and k.data_ptr() == base.data_ptr() + nq * hd * es and v.data_ptr() == base.data_ptr() + (nq + nkv) * hd * es
                 and q.stride(1) == hd and k.stride(1) == hd and v.stride(1) == hd):
             return None
-        qr = ext().rope_kv_append(base, re.cos_table, re.sin_table, kv.state.pos, nq, nkv, re.dimensions, re.interleaved,
+        qr = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), re.cos_table, re.sin_table, kv.state.pos, nq, nkv, re.dimensions, re.interleaved,
                                   kv.k, kv.v)
         if qr is None:
             return None
@@ -497,11 +529,17 @@ class ParallelSelfAttention(torch.nn.Module):
         attention_scores_manipulation: Optional[torch.Tensor] = None,
         attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True,
         max_seq_length: Optional[int] = None,
+        projected_base: Optional[torch.Tensor] = None,
     ) -> torch.Tensor:
+        """``projected_base``: the q/k/v projection of ``x`` already computed (``decode_norm_project``)."""
         b, s, _ = x.shape
         T = b * s
         hd = self.hidden_size_per_attention_head
-        q, k, v, base = self._project_base(x)
+        if projected_base is not None:
+            base = projected_base
+            q, k, v = self._split_base(base, T)
+        else:
+            q, k, v, base = self._project_base(x)
         lora_pending = self.lora_config is not None and not self.lora_merged_state
         lora_in_base = lora_pending and self._lora_into_base(x, base)
         if lora_in_base:  # fresh views of the updated GEMM output

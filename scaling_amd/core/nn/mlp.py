@@ -82,10 +82,9 @@ class ParallelSwiGLUMLP(torch.nn.Module):
             parallel_output=(topology.config.sequence_parallel if topology is not None else False), **kw
         )
 
-    def decode_forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> Optional[torch.Tensor]:
-        """``residual + self(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, TP 1, bias-free) as two
-        GEMV launches with fused epilogues -- gate/up GEMV + SwiGLU, down GEMV + residual add -- bit-identical to
-        the unfused GEMV / SwiGLU / add sequence; None when the fused path does not apply."""
+    def _decode_weights(self, x: torch.Tensor, residual: torch.Tensor) -> Optional[tuple[torch.Tensor, torch.Tensor]]:
+        """``([gate; up], down)`` weights for the decode GEMV path (<= 4 rows, no autograd graph, TP 1, bias-free,
+        GEMV-compatible layouts), None when it does not apply."""
         K = x.shape[-1]
         rows = x.numel() // K if K else 0
         if not (0 < rows <= 4 and use_native(x) and residual.shape == x.shape[:-1] + (self.dense_out.out_features,)):
@@ -98,13 +97,43 @@ class ParallelSwiGLUMLP(torch.nn.Module):
         if any(getattr(m, "bias_param", None) is not None for m in (self.dense_in, self.siglu_weight, self.dense_out)):
             return None
         w = adjacent_weights([self.dense_in.weight, self.siglu_weight.weight])
-        x2 = x.reshape(rows, K)
         wo = self.dense_out.weight
-        if (w is None or not ext().gemv_ok(x2, w) or wo.dtype != w.dtype or wo.stride(1) != 1 or wo.stride(0) % 8
-                or wo.shape[1] != w.shape[0] // 2 or wo.shape[1] % 8 or wo.data_ptr() % 16):
+        if (w is None or not ext().gemv_ok(x.reshape(rows, K), w) or wo.dtype != w.dtype or wo.stride(1) != 1
+                or wo.stride(0) % 8 or wo.shape[1] != w.shape[0] // 2 or wo.shape[1] % 8 or wo.data_ptr() % 16):
             return None
-        h = ext().gemv_swiglu(x2, w)
-        return ext().gemv_residual(h, self.dense_out.weight, residual.reshape(rows, -1)).view(residual.shape)
+        return w, wo
+
+    def decode_forward_residual(self, x: torch.Tensor, residual: torch.Tensor) -> Optional[torch.Tensor]:
+        """``residual + self(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, TP 1, bias-free) as two
+        GEMV launches with fused epilogues -- gate/up GEMV + SwiGLU, down GEMV + residual add -- bit-identical to
+        the unfused GEMV / SwiGLU / add sequence; None when the fused path does not apply."""
+        ws = self._decode_weights(x, residual)
+        if ws is None:
+            return None
+        rows = x.numel() // x.shape[-1]
+        h = ext().gemv_swiglu(x.reshape(rows, -1), ws[0])
+        return ext().gemv_residual(h, ws[1], residual.reshape(rows, -1)).view(residual.shape)
+
+    def decode_forward_norm(self, h: torch.Tensor, residual: torch.Tensor, norm: torch.nn.Module) -> Optional[torch.Tensor]:
+        """``s + self(norm(s))`` with ``s = residual + h`` (the post-attention residual add, RMSNorm and MLP of a
+        decode step) as two GEMV launches: the gate/up GEMV folds the add + RMSNorm into its pass over the weights
+        (the normalised row stays fp32 instead of being rounded to bf16) and applies SwiGLU, the down GEMV adds
+        ``s``.  None when the fused path does not apply."""
+        prologue = getattr(norm, "gemv_prologue", None)
+        nw = prologue() if prologue is not None else None
+        if nw is None or h.shape != residual.shape or not residual.is_contiguous() or not h.is_contiguous():
+            return None
+        ws = self._decode_weights(h, residual)
+        if ws is None:
+            return None
+        if torch.is_grad_enabled() and nw[0].requires_grad:
+            return None
+        rows = h.numel() // h.shape[-1]
+        h2 = h.reshape(rows, -1)
+        if not ext().gemv_norm_ok(h2, ws[0], nw[0]):
+            return None
+        s, a = ext().gemv_norm(h2, residual.reshape(rows, -1), nw[0], nw[1], ws[0], 2)
+        return ext().gemv_residual(a, ws[1], s).view(residual.shape)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         z = fused_column_linear(x, [self.dense_in, self.siglu_weight], self.topology)

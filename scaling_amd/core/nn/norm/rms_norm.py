@@ -44,3 +44,10 @@ class RMSNorm(torch.nn.Module):
         if self.topology is not None and self.topology.config.sequence_parallel:
             out = gather_from_sequence_parallel_region(out, topology=self.topology, tensor_parallel_output_grad=True)
         return s, out
+
+    def gemv_prologue(self) -> Optional[tuple[torch.Tensor, float]]:
+        """``(weight, eps)`` when this norm can run as the RMSNorm prologue of a decode GEMV (``ext().gemv_norm``):
+        the normalised rows must be consumed locally, i.e. no sequence-parallel gather after the norm."""
+        if self.topology is not None and self.topology.config.sequence_parallel:
+            return None
+        return self.weight, self.eps

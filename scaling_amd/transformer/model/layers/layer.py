@@ -16,6 +16,8 @@ from .embedding import _device
 
 # decode-sized MLP blocks on the fused GEMV epilogues (SwiGLU, residual add); SCALING_AMD_DECODE_FUSED=0 for A/B
 _DECODE_FUSED = os.environ.get("SCALING_AMD_DECODE_FUSED", "1") != "0"
+# decode-sized RMSNorms as prologues of the following GEMVs; SCALING_AMD_DECODE_NORM_GEMV=0 for A/B
+_DECODE_NORM_GEMV = _DECODE_FUSED and os.environ.get("SCALING_AMD_DECODE_NORM_GEMV", "1") != "0"
 
 
 class ZeroLayer(torch.nn.Module):
@@ -148,13 +150,26 @@ class TransformerLayer(TransformerLayerBaseIO):
         if (self.dropout_attention.p == 0.0 or not self.training) and not hasattr(self, "attn_adapter_name"):
             # residual stream through the fused norms: input_layernorm folds the residual-branch gradient into its
             # backward; post_attention_layernorm writes x + attn and norm(x + attn) in one pass
-            resid, normed = self.input_layernorm.forward_add(x.activations, None)
+            # (decode-sized rows: both norms run as prologues of the q/k/v and gate/up GEMVs instead)
+            proj = getattr(self.self_attention, "decode_norm_project", None) if _DECODE_NORM_GEMV else None
+            base = proj(x.activations, self.input_layernorm) if proj is not None else None
+            kw = {} if base is None else {"projected_base": base}
+            if base is None:
+                resid, normed = self.input_layernorm.forward_add(x.activations, None)
+            else:
+                resid = normed = x.activations
             h = self.self_attention(
                 normed, cumulative_seq_lengths=attn_args[1], position_ids=attn_args[2], use_cache=attn_args[3],
                 reset_cache=attn_args[4], cache_index=attn_args[5], attention_scores_manipulation=attn_args[6],
-                attentions_score_manipulation_log_additive=attn_args[7])
-            resid, normed = self.post_attention_layernorm.forward_add(resid, h)
-            act = self._mlp_tail(resid, normed)
+                attentions_score_manipulation_log_additive=attn_args[7], **kw)
+            act = None
+            if (_DECODE_NORM_GEMV and (self.dropout_mlp.p == 0.0 or not self.training)
+                    and not hasattr(self, "mlp_adapter_name")):
+                fused = getattr(self.mlp, "decode_forward_norm", None)
+                act = fused(h, resid, self.post_attention_layernorm) if fused is not None else None
+            if act is None:
+                resid, normed = self.post_attention_layernorm.forward_add(resid, h)
+                act = self._mlp_tail(resid, normed)
         else:
             act = self.mlp_block(self.attention_block(*attn_args))
         if st is not None and (self.layer_index + 1) in st.embedding_layers:

@@ -200,3 +200,37 @@ def test_gpu_graph_decode_matches_eager(stop_at):
     # a second graph generation (fresh capture over a re-prefilled cache) repeats itself exactly
     again = m.generate(20, input_tokens=prompt, stop_tokens=stops, use_cache=True, use_cuda_graph=True)
     assert again.completion_tokens == graph.completion_tokens
+
+
+def test_gpu_graph_decode_uses_fused_step_kernels(monkeypatch):
+    """The graph-decode step runs the fused decode kernels -- RoPE + K/V append in one launch, both RMSNorms as GEMV
+    prologues, SwiGLU / residual GEMV epilogues -- and not their unfused fallbacks (each path declines silently when
+    a layout check fails, so the test pins that they are taken on a Llama-style layer)."""
+    from scaling_amd.ops._ext import ext
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+    from scaling_amd.transformer.inference import TransformerInferenceModule
+    from scaling_amd.transformer.model.model import get_transformer_layer_specs
+
+    arch = TransformerArchitectureConfig(
+        vocab_size=256, hidden_size=256, num_layers=2, num_attention_heads=4, sequence_length=128, norm_type="rms",
+        mlp_type="swiglu", mlp_factor=2.0, precision="bfloat16", attention_num_kv_heads=2, attention_qkv_in_one=False,
+        relative_position_embedding_type="rotary_complex", masked_softmax={"kernel": "flash_attention"},
+        attention_bias=False, mlp_bias=False)  # Llama layout: the fused decode paths need bias-free projections
+    torch.manual_seed(0)
+    m = TransformerInferenceModule(get_transformer_layer_specs(arch), devices=(0,))
+    calls: dict = {}
+    mod = ext()
+    for name in ("rope_kv_append", "gemv_norm", "gemv_residual"):
+        fn = getattr(mod, name)
+
+        def wrapped(*a, _fn=fn, _name=name, **k):
+            out = _fn(*a, **k)
+            calls[_name] = calls.get(_name, 0) + (out is not None)
+            return out
+
+        monkeypatch.setattr(mod, name, wrapped)
+    m.generate(4, input_tokens=[3, 17, 42], stop_tokens=[], use_cache=True, use_cuda_graph=True)
+    # per captured layer step: one rope_kv_append, two gemv_norm (q/k/v, gate/up), one gemv_residual
+    assert calls.get("rope_kv_append", 0) >= 2, calls
+    assert calls.get("gemv_norm", 0) >= 4, calls
+    assert calls.get("gemv_residual", 0) >= 2, calls

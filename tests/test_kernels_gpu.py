@@ -803,6 +803,65 @@ def test_gemv_epilogues_bit_identical(rows, dtype):
     torch.testing.assert_close(h.float(), hf, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("rows", [1, 2, 4])
+@pytest.mark.parametrize("K", [4096, 520, 8192])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemv_norm_fused(rows, K, dtype):
+    """Decode GEMV with the RMSNorm (and its residual add) folded into the pass over the weights: the residual sum s
+    is bit-identical to add_rms_norm's, y matches fp32 math of norm + GEMV (plain / SwiGLU epilogues) and stays
+    within bf16 rounding of the unfused norm + GEMV kernels."""
+    from scaling_amd.ops import norm as norm_ops
+
+    torch.manual_seed(rows + K)
+    N, F = 264, 136
+    x = torch.randn(rows, K, device=DEV, dtype=dtype)
+    add = torch.randn(rows, K, device=DEV, dtype=dtype)
+    g = 1 + 0.1 * torch.randn(K, device=DEV, dtype=dtype)
+    w = torch.randn(N, K, device=DEV, dtype=dtype) / math.sqrt(K)
+    w2 = torch.randn(2 * F, K, device=DEV, dtype=dtype) / math.sqrt(K)
+    assert ext().gemv_norm_ok(x, w, g)
+
+    def rms(t):
+        t = t.float()
+        return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+
+    s, y = ext().gemv_norm(x, None, g, 1e-5, w, 0)
+    assert s.data_ptr() == x.data_ptr()
+    torch.testing.assert_close(y.float(), rms(x) @ w.float().t(), atol=2e-2, rtol=2e-2)
+    _, xn = norm_ops.add_rms_norm(x, None, g, 1e-5)
+    torch.testing.assert_close(y, ext().gemv(xn, w, None), atol=3e-2, rtol=3e-2)
+    s_ref, xn2 = norm_ops.add_rms_norm(add, x, g, 1e-5)  # the layer's order: residual + attention output
+    s, y2 = ext().gemv_norm(x, add, g, 1e-5, w2, 2)
+    assert torch.equal(s, s_ref)
+    nf = rms(s_ref)
+    hf = torch.nn.functional.silu(nf @ w2[:F].float().t()) * (nf @ w2[F:].float().t())
+    torch.testing.assert_close(y2.float(), hf, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(y2, ext().gemv_swiglu(xn2, w2), atol=3e-2, rtol=3e-2)
+    # deterministic: the same call twice is bit-identical (eager and graph decoding run the same kernel)
+    assert torch.equal(ext().gemv_norm(x, add, g, 1e-5, w2, 2)[1], y2)
+
+
+def test_decode_layer_norm_gemv_matches_unfused():
+    """The decode MLP block with the post-attention RMSNorm folded into the gate/up GEMV matches the unfused
+    add_rms_norm + GEMV-epilogue path within bf16 rounding, and writes the same residual stream."""
+    from scaling_amd.core.nn.mlp import ParallelSwiGLUMLP
+    from scaling_amd.core.nn.norm import RMSNorm, LayerNormConfig
+
+    torch.manual_seed(0)
+    H = 1024
+    mlp = ParallelSwiGLUMLP(H, 2.6875, bias=False, device=DEV, dtype=torch.bfloat16).requires_grad_(False)
+    norm = RMSNorm(H, DEV, LayerNormConfig(), dtype=torch.bfloat16).requires_grad_(False)
+    norm.weight.copy_(1 + 0.1 * torch.randn(H, device=DEV))
+    resid = torch.randn(1, 1, H, device=DEV, dtype=torch.bfloat16)
+    h = torch.randn(1, 1, H, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        out = mlp.decode_forward_norm(h, resid, norm)
+        assert out is not None
+        s, normed = norm.forward_add(resid, h)
+        ref = mlp.decode_forward_residual(normed, s)
+    torch.testing.assert_close(out.float(), ref.float(), atol=5e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("interleaved", [False, True])
 @pytest.mark.parametrize("rot_frac", [1.0, 0.5])
 def test_rope_kv_append_bit_identical(interleaved, rot_frac):

@@ -15,6 +15,7 @@ def short(name: str) -> str:
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         m = re.search(r"(Cijk_A\w{3}_B\w{3}).*?(MT\d+x\d+x\d+)", name)
         return f"GEMM {m.group(1)} {m.group(2)}" if m else "GEMM"
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
     return name[:90]
 
@@ -24,9 +25,14 @@ def main() -> None:
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--steps", type=int, default=1, help="divide totals by this many profiled steps")
+    ap.add_argument("--tail-ms", type=float, default=None,
+                    help="only kernels that start within the last this-many ms of the trace (e.g. a graph replay phase)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute("select name, start, end from kernels"))
+    if a.tail_ms is not None:
+        end = max(r[2] for r in rows)
+        rows = [r for r in rows if r[1] >= end - a.tail_ms * 1e6]
     tot = defaultdict(float)
     cnt = defaultdict(int)
     t0 = min(r[1] for r in rows)
