@@ -3,8 +3,8 @@
 // Token-by-token generation runs every linear layer at M = 1: the layer is a weight stream (2 bytes of W per
 // 2 FLOPs), and hipBLASLt's GEMM tiles move it at ~1.1 TB/s on the 7B decode step.  Here W is streamed once at
 // full width (cdna_hip_programming.md, "GEMV / M <= 16 decode weights": straight to VGPRs, deep unroll, late wait):
-//  * one wave per output row n, all M inputs at once; lanes split K in 16-byte pieces (8 elements), four pieces
-//    per lane in flight per trip (4 KiB per wave), fp32 FMAs;
+//  * one wave per output row n (or four waves splitting K, see gemv_kernel), all M inputs at once; lanes split K
+//    in 16-byte pieces (8 elements), four pieces per lane in flight per trip (4 KiB per wave), fp32 FMAs;
 //  * x is tiny (M x K) and re-read by every wave from L1/L2 (at M <= 4 its L1 traffic stays within the CU's
 //    load bandwidth);
 //  * one wave reduction per (row, input) at the end; bias added in fp32, one rounding to the output type.
@@ -39,14 +39,16 @@ struct NormArgs {
     float eps;
 };
 
+// Streams this wave's share of K -- pieces g0, g0 + GS, ... (GS = 64 x waves per row) -- of NR weight rows against
+// all M inputs; returns the wave-reduced dot products acc and (NORM) sums of squares ss.
 template <int M, int NR, typename E, bool NORM>
 __device__ __forceinline__ void gemv_rows(const E* __restrict__ x, int64_t ldx, const E* const (&w)[NR], int K,
-                                          int lane, float (&acc)[NR][M], const NormArgs<E>& na, bool write_sum) {
+                                          int g0, int GS, float (&acc)[NR][M], float (&ss)[M], const NormArgs<E>& na,
+                                          bool write_sum) {
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
         for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
-    float ss[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) ss[m] = 0.f;
     // one 8-element piece p of every input row against the weight pieces wv (NR rows)
@@ -77,30 +79,35 @@ __device__ __forceinline__ void gemv_rows(const E* __restrict__ x, int64_t ldx, 
                 for (int i = 0; i < 8; ++i) acc[r][m] = __builtin_fmaf(wv[r][i], xv[i], acc[r][m]);
         }
     };
-    constexpr int U = 4 / NR;
-    const int G = K >> 3;  // 8-element pieces per row
-    int g = lane;
-    for (; g + 64 * (U - 1) < G; g += 64 * U) {
+    constexpr int U = 4 / NR > 0 ? 4 / NR : 1;  // pieces per weight row per trip (4 KiB per wave)
+    const int G = K >> 3;                        // 8-element pieces per row
+    int g = g0;
+    for (; g + GS * (U - 1) < G; g += GS * U) {
         float wv[U][NR][8];
 #pragma unroll
         for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int u = 0; u < U; ++u) V8<E>::ld(w[r] + 8 * (g + 64 * u), wv[u][r]);
+            for (int u = 0; u < U; ++u) V8<E>::ld(w[r] + 8 * (g + GS * u), wv[u][r]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) piece(g + 64 * u, wv[u]);
+        for (int u = 0; u < U; ++u) piece(g + GS * u, wv[u]);
     }
-    for (; g < G; g += 64) {
-        float wv[NR][8];
+    if (g < G) {  // the ragged tail as ONE predicated trip
+        float wv[U][NR][8];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) V8<E>::ld(w[r] + 8 * g, wv[r]);
-        piece(g, wv);
+        for (int u = 0; u < U; ++u)
+            if (g + GS * u < G) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) V8<E>::ld(w[r] + 8 * (g + GS * u), wv[u][r]);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (g + GS * u < G) piece(g + GS * u, wv[u]);
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-        float rstd = 1.f;
-        if constexpr (NORM) rstd = rsqrtf(wave_sum(ss[m]) / K + na.eps);
+        if constexpr (NORM) ss[m] = wave_sum(ss[m]);
 #pragma unroll
-        for (int r = 0; r < NR; ++r) acc[r][m] = wave_sum(acc[r][m]) * rstd;
+        for (int r = 0; r < NR; ++r) acc[r][m] = wave_sum(acc[r][m]);
     }
 }
 
@@ -115,15 +122,19 @@ __device__ __forceinline__ float pick(const float (&a)[M], int lane) {
 }
 
 // RPW output rows per wave (consecutive rows r, r + 1): the NORM kernels take 2, which halves the per-weight-byte
-// work on x / add / gamma (every wave recomputes the normalised row for the pieces it streams)
-template <int M, int EPI, typename E, bool NORM, int RPW>
+// work on x / add / gamma (every wave recomputes the normalised row for the pieces it streams).
+// KS waves per row (1 or 4): with few output rows (N = 4096: o / down projections) one wave per row leaves the CUs
+// a quarter occupied, so the workgroup's four waves split K (interleaved 1 KiB slices, the workgroup streams
+// contiguous 4 KiB) and reduce through LDS in a fixed order.
+template <int M, int EPI, typename E, bool NORM, int RPW, int KS>
 __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int64_t ldx, const E* __restrict__ W,
                                                    int64_t ldw, const E* __restrict__ bias, const E* __restrict__ res,
                                                    int64_t ldr, E* __restrict__ y, int64_t ldy, int N, int K,
                                                    NormArgs<E> na) {
-    const int lane = threadIdx.x & 63;
-    const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-    if (row >= N) return;  // wave-uniform (N % RPW == 0)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int row = (blockIdx.x * (4 / KS) + wv / KS) * RPW;
+    const int kw = wv % KS;  // this wave's K slice
+    if (row >= N) return;    // wave-uniform (N % RPW == 0); workgroup-uniform when KS == 4
     constexpr int NS = EPI == EPI_SWIGLU ? 2 : 1;  // weight rows per output row
     constexpr int NR = NS * RPW;
     const E* w[NR];
@@ -132,8 +143,38 @@ __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int6
         w[q] = W + (int64_t)(row + q) * ldw;
         if constexpr (NS == 2) w[RPW + q] = W + (int64_t)(row + q + N) * ldw;  // up row F + n
     }
-    float acc[NR][M];
-    gemv_rows<M, NR, E, NORM>(x, ldx, w, K, lane, acc, na, NORM && row == 0);
+    float acc[NR][M], ss[M];
+    gemv_rows<M, NR, E, NORM>(x, ldx, w, K, lane + 64 * kw, 64 * KS, acc, ss, na, NORM && row == 0);  // row 0's waves write s
+    if constexpr (KS > 1) {
+        // partial sums of the K slices: waves 1..KS-1 -> LDS, wave 0 adds them in slice order
+        __shared__ float red[KS][NR + 1][M];
+        if (kw > 0 && lane == 0) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) red[kw][r][m] = acc[r][m];
+                red[kw][NR][m] = ss[m];
+            }
+        }
+        __syncthreads();
+        if (kw > 0) return;
+#pragma unroll
+        for (int k = 1; k < KS; ++k)
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc[r][m] += red[k][r][m];
+                ss[m] += red[k][NR][m];
+            }
+    }
+    if constexpr (NORM) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const float rstd = rsqrtf(ss[m] / K + na.eps);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) acc[r][m] *= rstd;
+        }
+    }
     if (lane < M) {
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -159,18 +200,38 @@ int rows_per_wave(bool norm, int N) {
     return (r == 2 && N % 2 == 0) ? 2 : 1;
 }
 
-template <int EPI, typename E, bool NORM, int RPW>
-void launch_r(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
+// waves per output row (cold-cache micro-benchmark, tools/gemv_bench.py): 4 for the NORM and SwiGLU kernels (their
+// per-piece work on x / gamma / two weight rows wants more waves in flight) and for long rows over few outputs
+// (the 4096 x 11008 down projection), 1 for the plain projections; SCALING_AMD_GEMV_KSPLIT=0/1 forces it off/on
+int waves_per_row(bool split) {
+    static const int env = [] {
+        const char* e = std::getenv("SCALING_AMD_GEMV_KSPLIT");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (env >= 0) return env > 0 ? 4 : 1;
+    return split ? 4 : 1;
+}
+
+template <int EPI, typename E, bool NORM, int RPW, int KS>
+void launch_k(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
               void* y, int64_t ldy, int N, int K, hipStream_t st, NormArgs<E> na) {
-    const dim3 grid((unsigned)((N + 4 * RPW - 1) / (4 * RPW))), block(256);
+    constexpr int RB = 4 / KS * RPW;  // output rows per workgroup
+    const dim3 grid((unsigned)((N + RB - 1) / RB)), block(256);
     const E *xp = (const E*)x, *wp = (const E*)W, *bp = (const E*)b, *rp = (const E*)r;
     E* yp = (E*)y;
     switch (M) {
-        case 1: hipLaunchKernelGGL((gemv_kernel<1, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
-        case 2: hipLaunchKernelGGL((gemv_kernel<2, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
-        case 3: hipLaunchKernelGGL((gemv_kernel<3, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
-        default: hipLaunchKernelGGL((gemv_kernel<4, EPI, E, NORM, RPW>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        case 1: hipLaunchKernelGGL((gemv_kernel<1, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        case 2: hipLaunchKernelGGL((gemv_kernel<2, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        case 3: hipLaunchKernelGGL((gemv_kernel<3, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
+        default: hipLaunchKernelGGL((gemv_kernel<4, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
     }
+}
+
+template <int EPI, typename E, bool NORM, int RPW>
+void launch_r(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
+              void* y, int64_t ldy, int N, int K, hipStream_t st, NormArgs<E> na) {
+    if (waves_per_row(NORM || EPI == EPI_SWIGLU || (N <= 8192 && K >= 2 * N)) == 4) launch_k<EPI, E, NORM, RPW, 4>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else launch_k<EPI, E, NORM, RPW, 1>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
 }
 
 template <int EPI, typename E, bool NORM>
