@@ -412,6 +412,31 @@ std::vector<at::Tensor> gemv_norm(const at::Tensor& x, c10::optional<at::Tensor>
                     (float)eps);
     return {s, y};
 }
+// graph-decode q/k/v step in ONE launch: q = RoPE(rms_norm(x) Wq^T) is returned, RoPE(rms_norm(x) Wk^T) and
+// rms_norm(x) Wv^T are written into the K / V cache rows at the device-side position pos (interleaved rotary pairs,
+// rotary dims rd of hd; x one token).  None when the operands do not fit (the caller runs gemv_norm + rope_kv_append).
+c10::optional<at::Tensor> gemv_norm_rope(const at::Tensor& x, const at::Tensor& gamma, double eps, const at::Tensor& W,
+                                         const at::Tensor& cosb, const at::Tensor& sinb, const at::Tensor& pos,
+                                         int64_t nq, int64_t nkv, int64_t rd, at::Tensor kc, at::Tensor vc) {
+    if (!gemv_norm_ok(x, W, gamma) || x.size(0) != 1) return c10::nullopt;
+    if (!(kc.is_cuda() && kc.dim() == 3 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes() &&
+          kc.size(1) == nkv && kc.scalar_type() == x.scalar_type() && vc.scalar_type() == x.scalar_type()))
+        return c10::nullopt;
+    const int64_t hd = kc.size(2);
+    if (hd % 2 || rd % 2 || rd > hd || W.size(0) != (nq + 2 * nkv) * hd) return c10::nullopt;
+    if (!(pos.is_cuda() && pos.scalar_type() == at::kLong && pos.numel() == 1 && cosb.scalar_type() == at::kFloat &&
+          sinb.scalar_type() == at::kFloat && cosb.is_contiguous() && sinb.is_contiguous() && cosb.size(-1) == rd / 2 &&
+          sinb.sizes() == cosb.sizes()))
+        return c10::nullopt;
+    const at::DeviceGuard g(x.device());
+    auto q = at::empty({1, nq, hd}, x.options());
+    GemvRope r{cosb.data_ptr<float>(), sinb.data_ptr<float>(), pos.data_ptr<int64_t>(), q.data_ptr(), kc.data_ptr(),
+               vc.data_ptr(), (int)nq, (int)nkv, (int)hd, (int)rd};
+    sa_launch::gemv(dt(x), 1, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), nullptr, nullptr, 0,
+                    (int)W.size(0), (int)W.size(1), cur_stream(), 3, nullptr, 0, gamma.data_ptr(), nullptr, nullptr,
+                    (float)eps, &r);
+    return q;
+}
 
 // ------------------------------------------------------------------ GEMM (weight gradient)
 // C[M, N] = A^T B (+ C if accumulate); A: [K, M], B: [K, N], C: [M, N], bf16, unit inner strides.
@@ -698,6 +723,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemv_residual", &gemv_residual, "y = x W^T + res for at most 4 rows (decode MLP-out + residual)");
     m.def("gemv_swiglu", &gemv_swiglu, "y = silu(x Wg^T) * (x Wu^T) for W = [Wg; Wu], at most 4 rows (decode)");
     m.def("gemv_norm_ok", &gemv_norm_ok, "whether gemv_norm supports these operands");
+    m.def("gemv_norm_rope", &gemv_norm_rope, "graph decode: rms_norm + q/k/v GEMV + interleaved RoPE + K/V cache append "
+          "in one launch; returns q or None");
     m.def("gemv_norm", &gemv_norm, "(s, gemv(rms_norm(s), W)) with s = x (+ add); epi 0 plain, 2 SwiGLU (decode)",
           py::arg("x"), py::arg("add"), py::arg("gamma"), py::arg("eps"), py::arg("W"), py::arg("epi") = 0);
     m.def("gemm_tn_ok", &gemm_tn_ok, "whether gemm_tn supports these operands");

@@ -29,7 +29,7 @@ using namespace sa;
 
 namespace {
 
-enum { EPI_NONE = 0, EPI_RES = 1, EPI_SWIGLU = 2 };
+enum { EPI_NONE = 0, EPI_RES = 1, EPI_SWIGLU = 2, EPI_ROPE = 3 };
 
 template <typename E>
 struct NormArgs {
@@ -37,6 +37,15 @@ struct NormArgs {
     const E* add;    // residual added before the norm ([M, K] contiguous) or nullptr
     E* sum;          // rnd(x + add), written by the wave of output row 0 when add != nullptr
     float eps;
+    // EPI_ROPE (one token, W = [q; k; v] heads of hd rows, interleaved rotary pairs = the wave's two rows):
+    // rotate q -> q_out, rotate k -> kc row pos, copy v -> vc row pos (rope_kv_append_kernel's arithmetic)
+    const float* cosb;
+    const float* sinb;
+    const int64_t* pos;
+    E* q_out;
+    E* kc;
+    E* vc;
+    int nq, nkv, hd, rd;
 };
 
 // Streams this wave's share of K -- pieces g0, g0 + GS, ... (GS = 64 x waves per row) -- of NR weight rows against
@@ -175,6 +184,29 @@ __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int6
             for (int r = 0; r < NR; ++r) acc[r][m] *= rstd;
         }
     }
+    if constexpr (EPI == EPI_ROPE) {
+        static_assert(RPW == 2, "EPI_ROPE: a wave's two rows are one rotary pair");
+        if (lane == 0) {
+            const float v0 = rnd<E>(acc[0][0]), v1 = rnd<E>(acc[1][0]);  // the projection's bf16 outputs
+            const int h = row / na.hd, d = row - h * na.hd;
+            const int64_t ps = na.pos[0];
+            float o0 = v0, o1 = v1;
+            E* dst;
+            if (h < na.nq + na.nkv) {
+                if (d < na.rd) {
+                    const float cs = na.cosb[ps * (na.rd / 2) + d / 2], sn = na.sinb[ps * (na.rd / 2) + d / 2];
+                    o0 = v0 * cs - v1 * sn;
+                    o1 = v1 * cs + v0 * sn;
+                }
+                dst = h < na.nq ? na.q_out + (int64_t)h * na.hd : na.kc + (ps * na.nkv + (h - na.nq)) * na.hd;
+            } else {
+                dst = na.vc + (ps * na.nkv + (h - na.nq - na.nkv)) * na.hd;
+            }
+            IO<E>::st(dst, d, o0);
+            IO<E>::st(dst, d + 1, o1);
+        }
+        return;
+    }
     if (lane < M) {
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -219,6 +251,10 @@ void launch_k(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, con
     const dim3 grid((unsigned)((N + RB - 1) / RB)), block(256);
     const E *xp = (const E*)x, *wp = (const E*)W, *bp = (const E*)b, *rp = (const E*)r;
     E* yp = (E*)y;
+    if constexpr (EPI == EPI_ROPE) {
+        hipLaunchKernelGGL((gemv_kernel<1, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na);
+        return;
+    }
     switch (M) {
         case 1: hipLaunchKernelGGL((gemv_kernel<1, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
         case 2: hipLaunchKernelGGL((gemv_kernel<2, EPI, E, NORM, RPW, KS>), grid, block, 0, st, xp, ldx, wp, ldw, bp, rp, ldr, yp, ldy, N, K, na); break;
@@ -237,8 +273,13 @@ void launch_r(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, con
 template <int EPI, typename E, bool NORM>
 void launch(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,
             void* y, int64_t ldy, int N, int K, hipStream_t st, NormArgs<E> na) {
-    if (rows_per_wave(NORM, N) == 2) launch_r<EPI, E, NORM, 2>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
-    else launch_r<EPI, E, NORM, 1>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    if constexpr (EPI == EPI_ROPE) {
+        if constexpr (NORM) launch_r<EPI, E, NORM, 2>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    } else if (rows_per_wave(NORM, N) == 2) {
+        launch_r<EPI, E, NORM, 2>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    } else {
+        launch_r<EPI, E, NORM, 1>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    }
 }
 
 template <int EPI, typename E>
@@ -251,7 +292,8 @@ void launch_n(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, con
 template <typename E>
 void launch_epi(int epi, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r,
                 int64_t ldr, void* y, int64_t ldy, int N, int K, hipStream_t st, const NormArgs<E>& na) {
-    if (epi == EPI_SWIGLU) launch_n<EPI_SWIGLU, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    if (epi == EPI_ROPE) launch_n<EPI_ROPE, E>(1, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
+    else if (epi == EPI_SWIGLU) launch_n<EPI_SWIGLU, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
     else if (epi == EPI_RES) launch_n<EPI_RES, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
     else launch_n<EPI_NONE, E>(M, x, ldx, W, ldw, b, r, ldr, y, ldy, N, K, st, na);
 }
@@ -259,17 +301,24 @@ void launch_epi(int epi, int M, const void* x, int64_t ldx, const void* W, int64
 }  // namespace
 
 namespace sa_launch {
-// epi 0: y = x W^T (+ b); 1: y = rnd(x W^T (+ b)) + res; 2: SwiGLU over W = [gate; up] (N = F output columns).
+// epi 0: y = x W^T (+ b); 1: y = rnd(x W^T (+ b)) + res; 2: SwiGLU over W = [gate; up] (N = F output columns);
+// 3 (with norm_w, one token): q/k/v projection + interleaved RoPE + K/V cache append (rope; y unused).
 // norm_w != nullptr: x is first replaced by rms_norm(x (+ norm_add), norm_w, eps) inside the same pass
 // (norm_add / norm_sum [M, K] contiguous; norm_sum receives x + norm_add).
 void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, void* y, int64_t ldy,
           int N, int K, hipStream_t st, int epi, const void* res, int64_t ldr, const void* norm_w, const void* norm_add,
-          void* norm_sum, float eps) {
+          void* norm_sum, float eps, const GemvRope* rope) {
+    const GemvRope z{};
+    const GemvRope& rp = rope ? *rope : z;
     if (dtype == DT_F16) {
-        const NormArgs<_Float16> na{(const _Float16*)norm_w, (const _Float16*)norm_add, (_Float16*)norm_sum, eps};
+        const NormArgs<_Float16> na{(const _Float16*)norm_w, (const _Float16*)norm_add, (_Float16*)norm_sum, eps,
+                                    rp.cosb, rp.sinb, rp.pos, (_Float16*)rp.q_out, (_Float16*)rp.kc, (_Float16*)rp.vc,
+                                    rp.nq, rp.nkv, rp.hd, rp.rd};
         launch_epi<_Float16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
     } else {
-        const NormArgs<u16> na{(const u16*)norm_w, (const u16*)norm_add, (u16*)norm_sum, eps};
+        const NormArgs<u16> na{(const u16*)norm_w, (const u16*)norm_add, (u16*)norm_sum, eps,
+                               rp.cosb, rp.sinb, rp.pos, (u16*)rp.q_out, (u16*)rp.kc, (u16*)rp.vc,
+                               rp.nq, rp.nkv, rp.hd, rp.rd};
         launch_epi<u16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
     }
 }

@@ -144,9 +144,16 @@ void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64
                        hipStream_t st);
 }
 
+// gemv.hip epi 3: interleaved RoPE of q / k and the K/V cache append at the device-side position
+struct GemvRope {
+    const float* cosb; const float* sinb; const int64_t* pos;
+    void* q_out; void* kc; void* vc;
+    int nq, nkv, hd, rd;
+};
 namespace sa_launch {
 // gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ b) for M <= 4 (decode-time linear layers), bf16 / fp16, K % 8 == 0
 void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, void* y, int64_t ldy,
           int N, int K, hipStream_t st, int epi = 0, const void* res = nullptr, int64_t ldr = 0,
-          const void* norm_w = nullptr, const void* norm_add = nullptr, void* norm_sum = nullptr, float eps = 0.f);
+          const void* norm_w = nullptr, const void* norm_add = nullptr, void* norm_sum = nullptr, float eps = 0.f,
+          const struct GemvRope* rope = nullptr);
 }  // namespace sa_launch

@@ -52,6 +52,8 @@ def repeat_kv(x: torch.Tensor, n_rep: int) -> torch.Tensor:
 
 # graph-decode step kernels (RoPE + K/V cache append in one launch); SCALING_AMD_DECODE_FUSED=0 for A/B
 _DECODE_FUSED = os.environ.get("SCALING_AMD_DECODE_FUSED", "1") != "0"
+# graph decode: RMSNorm + q/k/v GEMV + interleaved RoPE + K/V append as ONE launch (ext().gemv_norm_rope)
+_DECODE_ROPE_GEMV = _DECODE_FUSED and os.environ.get("SCALING_AMD_DECODE_ROPE_GEMV", "0") == "1"
 
 
 def get_max_seq_length(cumulative_seq_lengths: torch.Tensor) -> int:
@@ -389,11 +391,15 @@ class ParallelSelfAttention(torch.nn.Module):
             return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :]
         return self._views(base, T)
 
-    def decode_norm_project(self, x: torch.Tensor, norm: torch.nn.Module) -> Optional[torch.Tensor]:
+    def decode_norm_project(self, x: torch.Tensor, norm: torch.nn.Module, position_ids: Optional[torch.Tensor] = None,
+                            use_cache: bool = False, reset_cache: bool = False, cache_index: int = 0) -> Optional[dict]:
         """The q/k/v projection of ``norm(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, bias-free,
         no pending LoRA) as ONE GEMV launch that folds the RMSNorm into its pass over the weights
-        (``ext().gemv_norm``; the normalised row stays fp32); pass the result to ``forward(..., projected_base=...)``.  None when the fused
-        path does not apply (the caller runs the norm and the plain forward)."""
+        (``ext().gemv_norm``; the normalised row stays fp32).  Returns the keyword arguments to pass to ``forward``:
+        ``projected_base`` (the projection), or -- graph-captured decoding of one token with interleaved RoPE --
+        ``projected_step`` (q rotated, k rotated and v already appended to the static cache by the same launch,
+        ``ext().gemv_norm_rope``).  None when the fused path does not apply (the caller runs the norm and the plain
+        forward)."""
         prologue = getattr(norm, "gemv_prologue", None)
         nw = prologue() if prologue is not None and _DECODE_FUSED else None
         if nw is None or x.dim() != 3 or not use_native(x) or not x.is_contiguous():
@@ -414,8 +420,30 @@ class ParallelSelfAttention(torch.nn.Module):
         x2 = x.reshape(rows, K)
         if w is None or not ext().gemv_norm_ok(x2, w, nw[0]):
             return None
+        step = self._decode_norm_rope_step(x2, nw, w, position_ids, use_cache, reset_cache, cache_index)
+        if step is not None:
+            return {"projected_step": step}
         _, base = ext().gemv_norm(x2, None, nw[0], nw[1], w, 0)
-        return base.view(*x.shape[:-1], w.shape[0])
+        return {"projected_base": base.view(*x.shape[:-1], w.shape[0])}
+
+    def _decode_norm_rope_step(self, x2: torch.Tensor, nw: tuple, w: torch.Tensor, position_ids: Optional[torch.Tensor],
+                               use_cache: bool, reset_cache: bool, cache_index: int) -> Optional[tuple]:
+        """norm + q/k/v GEMV + RoPE + K/V append of one graph-decode token in one launch; None if not applicable."""
+        if not (_DECODE_ROPE_GEMV and use_cache and not reset_cache and x2.shape[0] == 1 and not self.key_query_norm
+                and not self.qkv_in_one):
+            return None
+        kv = self.cache.get(cache_index)
+        re = self.rotary_embedding
+        if not (isinstance(kv, StaticKVCache) and re is not None and re.interleaved and self.use_flash_attention):
+            return None
+        if position_ids is None or position_ids.numel() != 1 or position_ids.data_ptr() != kv.state.pos.data_ptr():
+            return None
+        q = ext().gemv_norm_rope(x2, nw[0], nw[1], w, re.cos_table, re.sin_table, kv.state.pos,
+                                 self.num_attention_heads_per_partition, self.num_kv_heads_per_partition, re.dimensions,
+                                 kv.k, kv.v)
+        if q is None:
+            return None
+        return q, kv.k, kv.v, kv.state.cu_k
 
     def _views(self, base: torch.Tensor, T: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         hd, nq, nkv = self.hidden_size_per_attention_head, self.num_attention_heads_per_partition, self.num_kv_heads_per_partition
@@ -530,40 +558,47 @@ class ParallelSelfAttention(torch.nn.Module):
         attentions_score_manipulation_log_additive: Union[bool, list[bool]] = True,
         max_seq_length: Optional[int] = None,
         projected_base: Optional[torch.Tensor] = None,
+        projected_step: Optional[tuple] = None,
     ) -> torch.Tensor:
-        """``projected_base``: the q/k/v projection of ``x`` already computed (``decode_norm_project``)."""
+        """``projected_base``: the q/k/v projection of ``x`` already computed; ``projected_step``: (q, k cache,
+        v cache, key cu_seqlens) of a graph-decode token whose RoPE and cache append are done
+        (both from ``decode_norm_project``)."""
         b, s, _ = x.shape
         T = b * s
         hd = self.hidden_size_per_attention_head
-        if projected_base is not None:
-            base = projected_base
-            q, k, v = self._split_base(base, T)
+        fused_append: Optional[tuple] = None
+        if projected_step is not None:  # graph decode: norm + q/k/v GEMV + RoPE + K/V append were one launch
+            q, k, v, cumulative_seq_lengths_key = projected_step
+            fused_append = projected_step
         else:
-            q, k, v, base = self._project_base(x)
-        lora_pending = self.lora_config is not None and not self.lora_merged_state
-        lora_in_base = lora_pending and self._lora_into_base(x, base)
-        if lora_in_base:  # fresh views of the updated GEMM output
-            q, k, v = self._views(base, T)
-        if not use_cache and not reset_cache and cumulative_seq_lengths_key is None:
-            fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length,
-                                               lora_in_base=lora_in_base)
-            if fused is not None:
-                return self._output(fused.reshape(b, s, -1))
-        if lora_pending and not lora_in_base:
-            q, k, v = self.apply_lora(x, q, k, v)
-        if self.key_query_norm:
-            assert self.norm_query is not None and self.norm_key is not None
-            q = all_shard(self.norm_query(all_concat(q, dim=1, topology=self.topology)), dim=1, topology=self.topology)
-            k = all_shard(self.norm_key(all_concat(k, dim=1, topology=self.topology)), dim=1, topology=self.topology)
-        fused_append = None
-        if use_cache and not reset_cache and T == 1 and not self.key_query_norm and _DECODE_FUSED:
-            fused_append = self._decode_rope_append(base, q, k, v, position_ids, cache_index)
-        if fused_append is not None:  # graph decode: RoPE + K/V cache append in one launch
-            q, k, v, cumulative_seq_lengths_key = fused_append
-        elif self.rotary_embedding is not None:
-            pos = position_ids.reshape(-1) if position_ids is not None else None
-            q = self.rotary_embedding.apply_tokens(q, pos, s)
-            k = self.rotary_embedding.apply_tokens(k, pos, s)
+            if projected_base is not None:
+                base = projected_base
+                q, k, v = self._split_base(base, T)
+            else:
+                q, k, v, base = self._project_base(x)
+            lora_pending = self.lora_config is not None and not self.lora_merged_state
+            lora_in_base = lora_pending and self._lora_into_base(x, base)
+            if lora_in_base:  # fresh views of the updated GEMM output
+                q, k, v = self._views(base, T)
+            if not use_cache and not reset_cache and cumulative_seq_lengths_key is None:
+                fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length,
+                                                   lora_in_base=lora_in_base)
+                if fused is not None:
+                    return self._output(fused.reshape(b, s, -1))
+            if lora_pending and not lora_in_base:
+                q, k, v = self.apply_lora(x, q, k, v)
+            if self.key_query_norm:
+                assert self.norm_query is not None and self.norm_key is not None
+                q = all_shard(self.norm_query(all_concat(q, dim=1, topology=self.topology)), dim=1, topology=self.topology)
+                k = all_shard(self.norm_key(all_concat(k, dim=1, topology=self.topology)), dim=1, topology=self.topology)
+            if use_cache and not reset_cache and T == 1 and not self.key_query_norm and _DECODE_FUSED:
+                fused_append = self._decode_rope_append(base, q, k, v, position_ids, cache_index)
+            if fused_append is not None:  # graph decode: RoPE + K/V cache append in one launch
+                q, k, v, cumulative_seq_lengths_key = fused_append
+            elif self.rotary_embedding is not None:
+                pos = position_ids.reshape(-1) if position_ids is not None else None
+                q = self.rotary_embedding.apply_tokens(q, pos, s)
+                k = self.rotary_embedding.apply_tokens(k, pos, s)
 
         if use_cache and fused_append is None:
             if not self.causal:

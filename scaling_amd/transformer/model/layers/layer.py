@@ -152,9 +152,10 @@ class TransformerLayer(TransformerLayerBaseIO):
             # backward; post_attention_layernorm writes x + attn and norm(x + attn) in one pass
             # (decode-sized rows: both norms run as prologues of the q/k/v and gate/up GEMVs instead)
             proj = getattr(self.self_attention, "decode_norm_project", None) if _DECODE_NORM_GEMV else None
-            base = proj(x.activations, self.input_layernorm) if proj is not None else None
-            kw = {} if base is None else {"projected_base": base}
-            if base is None:
+            kw = proj(x.activations, self.input_layernorm, attn_args[2], attn_args[3], attn_args[4],
+                      attn_args[5]) if proj is not None else None
+            if kw is None:
+                kw = {}
                 resid, normed = self.input_layernorm.forward_add(x.activations, None)
             else:
                 resid = normed = x.activations

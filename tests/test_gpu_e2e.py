@@ -203,8 +203,9 @@ def test_gpu_graph_decode_matches_eager(stop_at):
 
 
 def test_gpu_graph_decode_uses_fused_step_kernels(monkeypatch):
-    """The graph-decode step runs the fused decode kernels -- RoPE + K/V append in one launch, both RMSNorms as GEMV
-    prologues, SwiGLU / residual GEMV epilogues -- and not their unfused fallbacks (each path declines silently when
+    """The graph-decode step runs the fused decode kernels -- norm + q/k/v GEMV + RoPE + K/V append in one launch, the
+    post-attention norm folded into the gate/up GEMV, SwiGLU / residual GEMV epilogues -- and not their unfused
+    fallbacks (each path declines silently when
     a layout check fails, so the test pins that they are taken on a Llama-style layer)."""
     from scaling_amd.ops._ext import ext
     from scaling_amd.transformer.context.config import TransformerArchitectureConfig
@@ -220,7 +221,9 @@ def test_gpu_graph_decode_uses_fused_step_kernels(monkeypatch):
     m = TransformerInferenceModule(get_transformer_layer_specs(arch), devices=(0,))
     calls: dict = {}
     mod = ext()
-    for name in ("rope_kv_append", "gemv_norm", "gemv_residual"):
+    from scaling_amd.core.nn.attention import attention as attn_mod
+
+    for name in ("gemv_norm_rope", "rope_kv_append", "gemv_norm", "gemv_residual"):
         fn = getattr(mod, name)
 
         def wrapped(*a, _fn=fn, _name=name, **k):
@@ -230,7 +233,11 @@ def test_gpu_graph_decode_uses_fused_step_kernels(monkeypatch):
 
         monkeypatch.setattr(mod, name, wrapped)
     m.generate(4, input_tokens=[3, 17, 42], stop_tokens=[], use_cache=True, use_cuda_graph=True)
-    # per captured layer step: one rope_kv_append, two gemv_norm (q/k/v, gate/up), one gemv_residual
-    assert calls.get("rope_kv_append", 0) >= 2, calls
-    assert calls.get("gemv_norm", 0) >= 4, calls
+    # per captured layer step: one gemv_norm_rope (norm + q/k/v + RoPE + K/V append), one gemv_norm (norm + gate/up +
+    # SwiGLU), one gemv_residual (down + residual)
+    # (SCALING_AMD_DECODE_ROPE_GEMV=0: q/k/v GEMV with the norm folded in, then one RoPE + K/V append launch)
+    if attn_mod._DECODE_ROPE_GEMV:
+        assert calls.get("gemv_norm_rope", 0) >= 2 and calls.get("gemv_norm", 0) >= 2, calls
+    else:
+        assert calls.get("rope_kv_append", 0) >= 2 and calls.get("gemv_norm", 0) >= 4, calls
     assert calls.get("gemv_residual", 0) >= 2, calls

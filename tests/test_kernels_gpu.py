@@ -841,6 +841,38 @@ def test_gemv_norm_fused(rows, K, dtype):
     assert torch.equal(ext().gemv_norm(x, add, g, 1e-5, w2, 2)[1], y2)
 
 
+@pytest.mark.parametrize("rot_frac", [1.0, 0.5])
+def test_gemv_norm_rope_matches_unfused(rot_frac):
+    """Graph-decode q/k/v step in one launch (norm + GEMV + interleaved RoPE + K/V cache append at the device position)
+    against gemv_norm followed by rope_kv_append."""
+    torch.manual_seed(5)
+    nq, nkv, hd, K, cap = 8, 2, 128, 1024, 64
+    rd = int(hd * rot_frac)
+    half = rd // 2
+    inv = 1.0 / (10000 ** (torch.arange(0, half, device=DEV, dtype=torch.float32) / half))
+    ang = torch.arange(cap, device=DEV, dtype=torch.float32)[:, None] * inv[None]
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    x = torch.randn(1, K, device=DEV, dtype=torch.bfloat16)
+    g = 1 + 0.1 * torch.randn(K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn((nq + 2 * nkv) * hd, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    pos = torch.tensor([29], device=DEV, dtype=torch.long)
+    kc = torch.randn(cap, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    vc = torch.randn(cap, nkv, hd, device=DEV, dtype=torch.bfloat16)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    _, base = ext().gemv_norm(x, None, g, 1e-5, w, 0)
+    q_ref = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), cos, sin, pos, nq, nkv, rd, True, kc_ref, vc_ref)
+    q = ext().gemv_norm_rope(x, g, 1e-5, w, cos, sin, pos, nq, nkv, rd, kc, vc)
+    assert q is not None and q_ref is not None
+    torch.testing.assert_close(q, q_ref, atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(kc, kc_ref, atol=1e-2, rtol=1e-2)
+    assert torch.equal(vc, vc_ref)
+    other = torch.ones(cap, dtype=torch.bool, device=DEV)
+    other[29] = False
+    assert torch.equal(kc[other], kc_ref[other])  # only the position's row was written
+    assert ext().gemv_norm_rope(torch.randn(2, K, device=DEV, dtype=torch.bfloat16), g, 1e-5, w, cos, sin, pos, nq,
+                                nkv, rd, kc, vc) is None  # one token only
+
+
 def test_decode_layer_norm_gemv_matches_unfused():
     """The decode MLP block with the post-attention RMSNorm folded into the gate/up GEMV matches the unfused
     add_rms_norm + GEMV-epilogue path within bf16 rounding, and writes the same residual stream."""
