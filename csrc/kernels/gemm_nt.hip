@@ -1,0 +1,305 @@
+// Forward / input-gradient GEMM of a linear layer on gfx950:  C[M, N] = A[M, K] B[N, K]^T, both operands
+// k-contiguous (A: activations or the output gradient, B: the weight [out, in] for the forward, its cached transpose
+// W^T for the input gradient), bf16 in, fp32 accumulate, with fused epilogues:
+//   EPI_STORE       C = acc
+//   EPI_SWIGLU      the fused gate/up projection of a SwiGLU MLP: B = [W_gate; W_up] ([2F, K]); each 256-column tile
+//                   covers 128 features (gate and up rows interleaved in 16-row blocks as they are staged), so every
+//                   lane holds gate and up of the same (token, feature): z = [g | u] (the backward's input, optional)
+//                   and h = silu(g) * u are written directly (no separate SwiGLU pass over z)
+//   EPI_SWIGLU_BWD  the input gradient of the MLP's down projection, dh = dY W_down, consumed in registers: reads
+//                   g, u from z and writes dz = [dh u silu'(g) | dh silu(g)] (dh never goes to memory)
+// Numerics: every epilogue rounds the GEMM result to bf16 first and then applies exactly the arithmetic of the
+// stand-alone SwiGLU kernels (swiglu_rope.hip), so the fused and unfused paths agree.
+//
+// Structure (one 256x256 tile per workgroup, 4 waves = one per SIMD, each 128x128 of 16x16x32 MFMAs in AGPRs):
+//  * 64-deep k-stages, two LDS stage buffers of [256 rows][64 k] bf16 per operand (2 x 64 KiB);
+//  * LDS-DMA pieces (buffer_load ... lds) of 8 rows x 128 B: every lane group of 8 reads ONE full 128-B line
+//    (the previous 16-rows x 64-B pieces read half lines: twice the cache-line requests per byte);
+//  * image swizzle: 16-B chunk c of row r at c ^ ((r >> 1) & 7) -- every ds_read_b128 lane group of a fragment
+//    read hits 16 distinct 16-B bank slots (conflict-free), and the DMA source is permuted to match;
+//  * per stage t: sub-step 0 multiplies k 0-31 (registers F0) while reading k 32-63 (F1); wait for own reads and
+//    DMA, ONE barrier; sub-step 1 multiplies F1 while reading F0 of stage t+1 and issuing the DMA of stage t+2 into
+//    the buffer this stage just vacated.  The barrier both publishes stage t+1 and releases buffer t for restaging,
+//    so one barrier per 128 MFMAs (the 32-deep ring needed one per 64), and each DMA piece has two sub-steps
+//    (~128 MFMAs) to land.
+//  * grid: XCD-aware bijective remap, then 8-row groups of tiles (the 32 tiles resident on one XCD share A/B panels
+//    in its L2).
+// Reference op: F.linear at src/scaling/core/nn/linear/column_parallel_linear.py:151 / row_parallel_linear.py:158,
+// SwiGLU at src/scaling/core/nn/mlp.py:157-161.
+#include "common.h"
+#include "flash_attn.h"
+#include "launch.h"
+
+using namespace sa;
+
+namespace sa_gemm_nt {
+
+using fa::bf16x8;
+using fa::lds_void;
+
+constexpr int kImg = 256 * 64 * 2;  // one operand's stage image [256][64] bf16
+constexpr int kStage = 2 * kImg;   // A + B
+constexpr int kLds = 2 * kStage;   // two stages
+
+__device__ __forceinline__ void mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void hard_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
+                                                         const u16* __restrict__ B, int ldb, uint32_t b_bytes, int M,
+                                                         int N, int K, NtEpi ep) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tm = M / 256, tn = N / 256;
+    const int v = xcd_remap(blockIdx.x, tm * tn);
+    const int group = 8 * tn;
+    const int first_m = (v / group) * 8;
+    const int gm = min(tm - first_m, 8);
+    const int within = v % group;
+    const int m0 = (first_m + within % gm) * 256, nt = within / gm;
+    const int T = K / 64;
+
+    // ---- LDS-DMA: wave w stages pieces P = w + 4i (image rows 8P .. 8P+7) of each operand; lane -> (row lane >> 3,
+    // 16-B slot lane & 7), source chunk = slot ^ f(row), f = (row >> 1) & 7 = 4 (P & 1) + (lane >> 4) (piece-invariant)
+    const int prow = lane >> 3;
+    const int pch = (lane & 7) ^ ((((wave & 1) << 2) | (lane >> 4)) & 7);
+    const int va = (prow * lda + 8 * pch) * 2;
+    const int vb = (prow * ldb + 8 * pch) * 2;
+    const int abase = __builtin_amdgcn_readfirstlane((m0 + 8 * wave) * lda * 2);
+    const int astep = __builtin_amdgcn_readfirstlane(32 * lda * 2);
+    int brow0, bsteprows;
+    if constexpr (EPI == EPI_SWIGLU) {
+        // image rows 16 jb .. +15: jb even = gate rows, jb odd = up rows of features f0 + 16 (jb >> 1) ..; piece P = w + 4i
+        // has jb = P >> 1: gate/up by (w >> 1) & 1, feature block i, half (w & 1)
+        brow0 = ((wave >> 1) & 1) * ep.F + nt * 128 + (wave & 1) * 8;
+        bsteprows = 16;
+    } else {
+        brow0 = nt * 256 + 8 * wave;
+        bsteprows = 32;
+    }
+    const int bbase = __builtin_amdgcn_readfirstlane(brow0 * ldb * 2);
+    const int bstep = __builtin_amdgcn_readfirstlane(bsteprows * ldb * 2);
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    const i32x4 rsa = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(A)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(A) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(a_bytes), fa::kBufFlags};
+    const i32x4 rsb = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(B)),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(B) >> 32)) & 0xffff),
+                       (int)__builtin_amdgcn_readfirstlane(b_bytes), fa::kBufFlags};
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)smem));
+    // piece P (0..15; even: A piece P/2, odd: B piece P/2) of stage U into stage buffer BUF.  Inline asm so the
+    // waitcnt pass does not drain the pipeline in front of every ds_read (it cannot tell which LDS bytes a
+    // compiler-visible LDS-DMA writes); m0 is written in the statement that reads it.
+#define NT_PIECE(P, BUF, U)                                                                                       \
+    {                                                                                                             \
+        const int i_ = (P) >> 1;                                                                                  \
+        const uint32_t l_ = lds0 + (BUF) * kStage + (((P) & 1) ? kImg : 0) + (wave + 4 * i_) * 1024;             \
+        const int ku_ = (U) * 128;                                                                                \
+        if ((P) & 1)                                                                                              \
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
+                         "v"(vb), "s"(rsb), "s"(bbase + i_ * bstep + ku_)                                          \
+                         : "m0");                                                                                 \
+        else                                                                                                      \
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
+                         "v"(va), "s"(rsa), "s"(abase + i_ * astep + ku_)                                          \
+                         : "m0");                                                                                 \
+    }
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- fragments: lane l holds row 16i + (l & 15) of its wave's 128 rows, k chunk 4h + (l >> 4) of the stage;
+    // stored chunk = c ^ f(r), f = ((l & 15) >> 1).  One opaque VGPR per (buffer, half, operand); fragment i in the
+    // ds_read immediate (i * 2048 + the B image's 32 KiB < 64 KiB).
+    int oa[2][2], ob[2][2];
+    {
+        const int r = lane & 15, g = lane >> 4, f = r >> 1;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int lo = r * 128 + 16 * ((g ^ f) ^ (4 * h));
+                oa[s][h] = s * kStage + wm * 128 * 128 + lo;
+                ob[s][h] = s * kStage + kImg + wn * 128 * 128 + lo;
+                asm volatile("" : "+v"(oa[s][h]), "+v"(ob[s][h]));
+            }
+    }
+    auto frag = [&](int off, int i) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(smem + off + i * 2048); };
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+    // sub-step 0 of stage U (buffer BUF): MFMAs on F0, F1 of the same stage read one fragment per 3 MFMAs over the
+    // first 48 (retired well before the waits); then own
+    // reads retired, own DMA landed (stage U+1), barrier
+#define NT_SUB0(BUF)                                                                                             \
+    {                                                                                                            \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {            \
+            mfma(acc[i][j], fb0[j], fa0[i]);                                                                     \
+            const int m_ = i * 8 + j;                                                                            \
+            if (m_ % 3 == 1 && m_ < 48) {                                                                        \
+                const int f_ = m_ / 3;                                                                           \
+                if (f_ < 8) fb1[f_] = frag(ob[BUF][1], f_);                                                      \
+                else fa1[f_ - 8] = frag(oa[BUF][1], f_ - 8);                                                     \
+            }                                                                                                    \
+        }                                                                                                        \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
+        wait_vm<0>();                                                                                            \
+        hard_barrier();                                                                                          \
+    }
+    // sub-step 1 of stage U: MFMAs on F1; F0 of stage U+1 from the other buffer (NEXT), DMA of stage U+2 into BUF
+    // (PIECES) one piece per 4 MFMAs
+#define NT_SUB1(BUF, U, NEXT, PIECES)                                                                            \
+    {                                                                                                            \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {            \
+            mfma(acc[i][j], fb1[j], fa1[i]);                                                                     \
+            const int m_ = i * 8 + j;                                                                            \
+            if ((NEXT) && m_ % 3 == 1 && m_ < 48) {                                                              \
+                const int f_ = m_ / 3;                                                                           \
+                if (f_ < 8) fb0[f_] = frag(ob[(BUF) ^ 1][0], f_);                                                \
+                else fa0[f_ - 8] = frag(oa[(BUF) ^ 1][0], f_ - 8);                                               \
+            }                                                                                                    \
+            if ((PIECES) && (m_ & 3) == 3) NT_PIECE(m_ >> 2, BUF, (U) + 2)                                      \
+        }                                                                                                        \
+    }
+
+    // prologue: stages 0 and 1 in flight, stage 0 landed, barrier, F0 of stage 0
+#pragma unroll
+    for (int p = 0; p < 16; ++p) NT_PIECE(p, 0, 0)
+#pragma unroll
+    for (int p = 0; p < 16; ++p) NT_PIECE(p, 1, 1)
+    wait_vm<16>();
+    hard_barrier();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+        if (f < 8) fb0[f] = frag(ob[0][0], f);
+        else fa0[f - 8] = frag(oa[0][0], f - 8);
+    }
+    int u = 0;
+    for (; u < T - 2; u += 2) {  // T even (K % 128 == 0, checked by the dispatcher)
+        NT_SUB0(0)
+        NT_SUB1(0, u, true, true)
+        NT_SUB0(1)
+        NT_SUB1(1, u + 1, true, true)
+    }
+    NT_SUB0(0)
+    NT_SUB1(0, u, true, false)
+    NT_SUB0(1)
+    NT_SUB1(1, u + 1, false, false)
+#undef NT_SUB0
+#undef NT_SUB1
+#undef NT_PIECE
+    wait_vm<0>();
+    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    // ---- epilogue: acc[i][j][e] = C[m0 + 128 wm + 16 i + (lane & 15)][tile col 128 wn + 16 j + 4 (lane >> 4) + e]
+    const int r = lane & 15, q4 = 4 * (lane >> 4);
+    if constexpr (EPI == EPI_STORE) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            u16* cp = ep.C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ep.ldc + nt * 256 + 128 * wn + q4;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                u16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e]);
+                *reinterpret_cast<u16x4*>(cp + 16 * j) = o;
+            }
+        }
+    } else if constexpr (EPI == EPI_SWIGLU) {
+        // j = 2 jj: gate, j = 2 jj + 1: up of features nt * 128 + 64 wn + 16 jj + q4 + e
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t row = m0 + 128 * wm + 16 * i + r;
+            const int f = nt * 128 + 64 * wn + q4;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                u16x4 gz, uz, hz;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    gz[e] = f2bf(acc[i][2 * jj][e]);
+                    uz[e] = f2bf(acc[i][2 * jj + 1][e]);
+                    hz[e] = f2bf(round_bf(silu_f(bf2f(gz[e]))) * bf2f(uz[e]));
+                }
+                if (ep.C) {
+                    *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + f + 16 * jj) = gz;
+                    *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + ep.F + f + 16 * jj) = uz;
+                }
+                *reinterpret_cast<u16x4*>(ep.H + row * ep.ldh + f + 16 * jj) = hz;
+            }
+        }
+    } else {  // EPI_SWIGLU_BWD: tile column = feature
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t row = m0 + 128 * wm + 16 * i + r;
+            const u16* zp = ep.Z + row * ep.ldz + nt * 256 + 128 * wn + q4;
+            u16* dp = ep.C + row * ep.ldc + nt * 256 + 128 * wn + q4;
+            u16x4 gz[8], uz[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                gz[j] = *reinterpret_cast<const u16x4*>(zp + 16 * j);
+                uz[j] = *reinterpret_cast<const u16x4*>(zp + ep.F + 16 * j);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                u16x4 da, db;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float g = round_bf(acc[i][j][e]);
+                    const float av = bf2f(gz[j][e]), bv = bf2f(uz[j][e]);
+                    const float sig = 1.f / (1.f + __expf(-av));
+                    const float s = av * sig;
+                    db[e] = f2bf(g * round_bf(s));
+                    const float ds = g * bv;
+                    da[e] = f2bf(ds * (sig * (1.f + av * (1.f - sig))));
+                }
+                *reinterpret_cast<u16x4*>(dp + 16 * j) = da;
+                *reinterpret_cast<u16x4*>(dp + ep.F + 16 * j) = db;
+            }
+        }
+    }
+}
+template __global__ void gemm_nt_kernel<EPI_STORE>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
+                                                   uint32_t, int, int, int, NtEpi);
+template __global__ void gemm_nt_kernel<EPI_SWIGLU>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
+                                                    uint32_t, int, int, int, NtEpi);
+template __global__ void gemm_nt_kernel<EPI_SWIGLU_BWD>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
+                                                        int, uint32_t, int, int, int, NtEpi);
+
+}  // namespace sa_gemm_nt
+
+namespace sa_launch {
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+    return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+           lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
+           (M / 256) * (N / 256) < (int64_t(1) << 31);
+}
+void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+               const NtEpi& ep, hipStream_t st) {
+    using namespace sa_gemm_nt;
+    const int nwg = (int)((M / 256) * (N / 256));
+    const uint32_t ab = (uint32_t)(M * lda * 2), bb = (uint32_t)(N * ldb * 2);
+#define SA_NT_LAUNCH(E)                                                                                         \
+    hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab,        \
+                       (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
+    if (epi == EPI_SWIGLU) SA_NT_LAUNCH(EPI_SWIGLU);
+    else if (epi == EPI_SWIGLU_BWD) SA_NT_LAUNCH(EPI_SWIGLU_BWD);
+    else SA_NT_LAUNCH(EPI_STORE);
+#undef SA_NT_LAUNCH
+}
+}  // namespace sa_launch

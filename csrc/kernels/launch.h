@@ -51,18 +51,25 @@ void transpose_u16(const void* in, int64_t ld_in, void* out, int64_t R, int64_t 
 }  // namespace sa_launch
 
 namespace sa_launch {
-// gemm.hip: C[M, N] (+)= A^T B, A [K, M] / B [K, N] row-major (k-major operands), bf16
-void gemm_set_variant(int v);
-int gemm_get_variant();
-bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
-void gemm_nt(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-             int64_t K, bool beta, hipStream_t st, uint64_t* timing_dbg = nullptr);
-void gemm_tn_timing(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-                    int64_t K, uint64_t* dbg, hipStream_t st);
+// gemm.hip: C[M, N] (+)= A^T B, A [K, M] / B [K, N] row-major (k-major operands), bf16 (weight gradient)
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_blocks, int& split);
 void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
              int64_t K, bool beta, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr);
+}  // namespace sa_launch
+
+// gemm_nt.hip: C[M, N] = A[M, K] B[N, K]^T (bf16, k-contiguous operands) with fused epilogues
+enum { EPI_STORE = 0, EPI_SWIGLU = 1, EPI_SWIGLU_BWD = 2 };
+struct NtEpi {
+    uint16_t* C; int64_t ldc;        // STORE: C; SWIGLU: z = [g | u] [M, 2F] (nullptr: not written); SWIGLU_BWD: dz [M, 2F]
+    uint16_t* H; int64_t ldh;        // SWIGLU: h = silu(g) u [M, F]
+    const uint16_t* Z; int64_t ldz;  // SWIGLU_BWD: z
+    int F;                           // SwiGLU intermediate features
+};
+namespace sa_launch {
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+               const NtEpi& ep, hipStream_t st);
 }  // namespace sa_launch
 
 // flash attention (bf16, head dim 32/64/128)

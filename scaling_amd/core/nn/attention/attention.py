@@ -400,6 +400,8 @@ class ParallelSelfAttention(torch.nn.Module):
         ``projected_step`` (q rotated, k rotated and v already appended to the static cache by the same launch,
         ``ext().gemv_norm_rope``).  None when the fused path does not apply (the caller runs the norm and the plain
         forward)."""
+        if not use_cache or reset_cache:  # real decode steps only (see TransformerLayer.forward)
+            return None
         prologue = getattr(norm, "gemv_prologue", None)
         nw = prologue() if prologue is not None and _DECODE_FUSED else None
         if nw is None or x.dim() != 3 or not use_native(x) or not x.is_contiguous():

@@ -6,7 +6,6 @@ reference implementations that live next to each op.
 """
 from __future__ import annotations
 
-import os
 from types import ModuleType
 from typing import Optional
 
@@ -26,9 +25,6 @@ def ext() -> ModuleType:
                 "or python -m scaling_amd._build)"
             ) from e
         _EXT = _C
-        v = os.environ.get("SCALING_AMD_GEMM_VARIANT")  # weight-gradient GEMM pipeline (benchmarking hook)
-        if v:
-            _EXT.gemm_set_variant(int(v))
     return _EXT
 
 

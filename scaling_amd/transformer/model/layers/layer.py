@@ -151,7 +151,10 @@ class TransformerLayer(TransformerLayerBaseIO):
             # residual stream through the fused norms: input_layernorm folds the residual-branch gradient into its
             # backward; post_attention_layernorm writes x + attn and norm(x + attn) in one pass
             # (decode-sized rows: both norms run as prologues of the q/k/v and gate/up GEMVs instead)
-            proj = getattr(self.self_attention, "decode_norm_project", None) if _DECODE_NORM_GEMV else None
+            # only on real decode steps (a cached step after the prompt): the fold keeps the normalised row in fp32, so
+            # a short prompt, eval or scoring batch must take the same norm + GEMM path as any longer input
+            decode_step = _DECODE_NORM_GEMV and st is not None and st.use_cache and not st.reset_cache
+            proj = getattr(self.self_attention, "decode_norm_project", None) if decode_step else None
             kw = proj(x.activations, self.input_layernorm, attn_args[2], attn_args[3], attn_args[4],
                       attn_args[5]) if proj is not None else None
             if kw is None:
@@ -164,7 +167,7 @@ class TransformerLayer(TransformerLayerBaseIO):
                 reset_cache=attn_args[4], cache_index=attn_args[5], attention_scores_manipulation=attn_args[6],
                 attentions_score_manipulation_log_additive=attn_args[7], **kw)
             act = None
-            if (_DECODE_NORM_GEMV and (self.dropout_mlp.p == 0.0 or not self.training)
+            if (decode_step and (self.dropout_mlp.p == 0.0 or not self.training)
                     and not hasattr(self, "mlp_adapter_name")):
                 fused = getattr(self.mlp, "decode_forward_norm", None)
                 act = fused(h, resid, self.post_attention_layernorm) if fused is not None else None

@@ -485,23 +485,12 @@ def test_flash_attention_deterministic():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (512, 768, 384), (1024, 512, 1024)])
-def test_gemm_tn(M, N, K, accumulate, variant):
-    """Weight-gradient GEMM C (+)= A^T B against an fp32 reference, incl. strided (sliced) operands; pipeline
-    variants 2 (32x32x16 MFMA), 4 (16x16x32 MFMA), 5 (three B buffers), 6 (no ping-pong), 7 (one wave per
-    SIMD, register-staged), 8 (one wave per SIMD, two LDS-DMA stages) and the four-slot ring 9-12 (10 is the
-    default; K = 320 is an odd number of 64-deep tiles, which the ring hands to variant 2)."""
-    prev = ext().gemm_get_variant()
-    ext().gemm_set_variant(variant)
-    try:
-        _gemm_tn_case(M, N, K, accumulate)
-    finally:
-        ext().gemm_set_variant(prev)
-
-
-def _gemm_tn_case(M, N, K, accumulate):
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024), (1280, 512, 640)])
+def test_gemm_tn(M, N, K, accumulate):
+    """Weight-gradient GEMM C (+)= A^T B (four-slot ring kernel) against an fp32 reference, incl. a strided (sliced)
+    A; 1280 x 512 = 10 tiles exercises the split-K tail on a 256-CU part only when the grid is ragged, the K = 640
+    case an odd number of 128-deep pairs per split; K not a multiple of 128 is rejected (hipBLASLt fallback)."""
     torch.manual_seed(5)
     A_full = torch.randn(K, M + 64, device=DEV, dtype=torch.bfloat16)
     A = A_full[:, 64:]  # row stride M + 64, 128-B aligned start
@@ -513,25 +502,61 @@ def _gemm_tn_case(M, N, K, accumulate):
     ref = A.float().t() @ B.float() + (C0.float() if accumulate else 0)
     torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
     assert not ext().gemm_tn_ok(A[:, :200], B, C[:200])
+    assert not ext().gemm_tn_ok(A[:64], B[:64], C)
 
 
-@pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2)])
-def test_gemm_nt(M, N, K, accumulate):
-    """Forward / dgrad GEMM C (+)= A B^T (ring kernel, ds_read_b128 fragments) against an fp32 reference, with a
-    strided (sliced) A and an asymmetric B."""
+def test_gemm_nt(M, N, K):
+    """Forward / dgrad GEMM C = A B^T (64-deep staged kernel, csrc/kernels/gemm_nt.hip) against an fp32 reference,
+    with a strided (sliced) A and an asymmetric B."""
     torch.manual_seed(7)
     A_full = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
     A = A_full[:, 64:]
     B = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * torch.linspace(0.5, 1.5, K, device=DEV).to(torch.bfloat16)
-    C0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
-    C = C0.clone()
-    assert ext().gemm_nt_ok(A, B, C)
-    ext().gemm_nt(A, B, C, accumulate)
-    ref = A.float() @ B.float().t() + (C0.float() if accumulate else 0)
+    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert ext().gemm_nt_ok(A, B)
+    ext().gemm_nt(A, B, C)
+    ref = A.float() @ B.float().t()
     torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
-    assert not ext().gemm_nt_ok(A[:200], B, C[:200])
-    assert not ext().gemm_nt_ok(A[:, : K - 64], B[:, : K - 64], C)
+    assert not ext().gemm_nt_ok(A[:200], B)
+    assert not ext().gemm_nt_ok(A[:, : K - 64], B[:, : K - 64])
+
+
+@pytest.mark.parametrize("M,F,K", [(256, 128, 128), (512, 384, 256), (1024, 1024, 512)])
+def test_gemm_nt_swiglu_epilogues(M, F, K):
+    """Fused SwiGLU epilogues of the NT GEMM: forward (z = x [W_g; W_u]^T, h = silu(g) u) and backward
+    (dz = swiglu_bwd(dY W_down, z)) are bit-identical to the unfused GEMM + SwiGLU kernels, and match an fp32
+    reference of the composite op."""
+    torch.manual_seed(11)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
+    z = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
+    h = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    assert ext().gemm_nt_swiglu_ok(x, w)
+    ext().gemm_nt_swiglu(x, w, z, h)
+    z_ref = torch.empty_like(z)
+    ext().gemm_nt(x, w, z_ref)
+    assert torch.equal(z, z_ref)
+    assert torch.equal(h, ext().swiglu_fwd(z_ref[:, :F], z_ref[:, F:]))
+    zf = x.float() @ w.float().t()
+    torch.testing.assert_close(h.float(), torch.nn.functional.silu(zf[:, :F]) * zf[:, F:], atol=3e-2, rtol=3e-2)
+    h2 = torch.empty_like(h)
+    ext().gemm_nt_swiglu(x, w, None, h2)  # inference form: z not written
+    assert torch.equal(h, h2)
+    H = 256
+    dy = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    wd = torch.randn(H, F, device=DEV, dtype=torch.bfloat16) / math.sqrt(F)
+    wdt = wd.t().contiguous()
+    dz = torch.empty_like(z)
+    ext().gemm_nt_swiglu_bwd(dy, wdt, z, dz)
+    dh = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    ext().gemm_nt(dy, wdt, dh)
+    (dz_ref,) = ext().swiglu_bwd(dh, z[:, :F], z[:, F:], True)
+    assert torch.equal(dz, dz_ref)
+    g, u = z[:, :F].float().requires_grad_(), z[:, F:].float().requires_grad_()
+    (torch.nn.functional.silu(g) * u).backward(dy.float() @ wd.float())
+    torch.testing.assert_close(dz[:, :F].float(), g.grad, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(dz[:, F:].float(), u.grad, atol=3e-2, rtol=3e-2)
 
 
 # ---------------------------------------------------------------- masked softmax / activations / dropout

@@ -1,4 +1,4 @@
-"""Runs the forward GEMM ring kernel (gemm_nt) at one shape a few times (a short program for rocprofv3 --pmc).
+"""Runs the forward GEMM kernel (gemm_nt) at one shape a few times (a short program for rocprofv3 --pmc).
 
     python tools/gemm_nt_one.py M N K [iters]
 """
@@ -16,6 +16,6 @@ a = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
 b = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(iters):
-    ext().gemm_nt(a, b, c, False)
+    ext().gemm_nt(a, b, c)
 torch.cuda.synchronize()
 print("done", M, N, K, iters)
