@@ -73,6 +73,10 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--lora", action="store_true",
                    help="LoRA finetune path (BASELINE #5): q/k/v/dense adapters trained, base weights frozen")
     p.add_argument("--lora-rank", type=int, default=64)
+    p.add_argument("--preset", type=str, default=None, choices=sorted(PRESETS),
+                   help="BASELINE.json layouts: baseline3 = TP2 x DP(N/2) ZeRO-1 + SP, baseline4 = TP2 x PP2 x DP(N/4) "
+                        "1F1B + activation checkpointing + SP, baseline5 = LoRA TP1 x DP(N) ZeRO-1 (overrides the "
+                        "layout flags it names; see PRESETS)")
     p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo", "gloo-gpu"],
                    help="gloo = CPU processes (plumbing mode, no GPU); gloo-gpu = rehearsal: GPU ranks (several "
                         "may share one GPU) with gloo collectives standing in for RCCL")
@@ -83,7 +87,34 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
     p.add_argument("--launch-timeout", type=float, default=3000.0, help="launcher: kill all ranks after this many s")
-    return p.parse_args(argv)
+    return apply_preset(p.parse_args(argv))
+
+
+# BASELINE.json configs 3-5 (the 8-GPU layouts; any N the layout divides).  Values override the corresponding flags.
+PRESETS: dict[str, dict[str, Any]] = {
+    # "Llama-2-7B-shape TP=2 PP=1 DP=4 bf16 + ZeRO-1": Megatron-SP inside the TP pair (reduce-scatter / all-gather
+    # instead of all-reduce, activations sharded), row-parallel GEMMs overlapped with their collective in 4 pieces
+    "baseline3": {"tp": 2, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": True, "tp_comm_chunks": 4,
+                  "activation_checkpointing": "disabled", "lora": False, "zero": 1},
+    # "TP=2 PP=2 DP=2 (full 3D parallel, 1F1B pipeline) with activation checkpointing": 4 micro-batches of 4 keep the
+    # two-stage pipe 4/5 busy; per-layer checkpointing as the reference's every_layer
+    "baseline4": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True, "tp_comm_chunks": 4,
+                  "activation_checkpointing": "every_layer", "lora": False, "zero": 1},
+    # "7B + LoRA fine-tune path, TP=1 PP=1 DP=8 ZeRO-1 (PEFT adapters exercised)"
+    "baseline5": {"tp": 1, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": False, "tp_comm_chunks": 1,
+                  "activation_checkpointing": "disabled", "lora": True, "zero": 1},
+}
+
+
+def apply_preset(a: argparse.Namespace) -> argparse.Namespace:
+    """Overrides the layout flags of ``a`` with its ``--preset`` (if any) and checks that the GPU count fits."""
+    if a.preset is None:
+        return a
+    for k, v in PRESETS[a.preset].items():
+        setattr(a, k, v)
+    if a.gpus % (a.tp * a.pp) != 0:
+        raise SystemExit(f"bench.py: --preset {a.preset} needs a multiple of {a.tp * a.pp} GPUs (got {a.gpus})")
+    return a
 
 
 def _env_int(k: str, d: int) -> int:
@@ -340,6 +371,7 @@ def _worker(a: argparse.Namespace) -> None:
                 "global_batch": gbs,
                 "seq_len": a.seq_len,
                 "parallelism": parallelism,
+                "preset": a.preset,
                 "micro_batch": a.micro_batch,
                 "grad_acc": a.grad_acc,
                 "loss": None if last is None else last.loss,

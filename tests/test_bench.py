@@ -79,3 +79,36 @@ def test_bench_tp_comm_chunks_gloo(sp):
         est = res["config"]["comm_estimate"]
         assert est["tp_bytes"] > 0 and est["dp_bytes"] == 0 and est["pp_bytes"] == 0
     assert losses["2"] == pytest.approx(losses["1"], rel=1e-5)
+
+
+@pytest.mark.parametrize("preset,gpus,tp,pp,dp,acc,ac,sp,lora", [
+    ("baseline3", 8, 2, 1, 4, 1, "disabled", True, False),
+    ("baseline4", 8, 2, 2, 2, 4, "every_layer", True, False),
+    ("baseline5", 8, 1, 1, 8, 1, "disabled", False, True),
+    ("baseline3", 4, 2, 1, 2, 1, "disabled", True, False),
+])
+def test_bench_preset_layouts(preset, gpus, tp, pp, dp, acc, ac, sp, lora):
+    """``--preset`` pins BASELINE.json configs 3-5 to their topology (TP x PP x DP, ZeRO-1, activation
+    checkpointing, sequence parallelism, LoRA) for any GPU count the layout divides."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = bench._args(["--gpus", str(gpus), "--preset", preset])
+    t = bench._config_dict(a, gpus, 0, 0)["topology"]
+    assert (t["model_parallel_size"], t["pipe_parallel_size"], t["data_parallel_size"]) == (tp, pp, dp)
+    assert t["gradient_accumulation_steps"] == acc and t["activation_checkpointing_type"] == ac
+    assert t["sequence_parallel"] is sp and bool(a.lora) is lora and a.zero == 1
+    cfg = bench._config_dict(a, gpus, 0, 0)
+    assert ("lora_config" in cfg["transformer_architecture"]) is lora
+    with pytest.raises(SystemExit):
+        bench._args(["--gpus", "1", "--preset", "baseline4"])
+
+
+def test_bench_preset_runs_gloo():
+    """The TP2 x PP2 preset (BASELINE #4) end to end on 4 CPU ranks; the JSON names the preset."""
+    r = _run(["--gpus", "4", "--preset", "baseline4", "--model", "llama_tiny", "--backend", "gloo", "--seq-len", "64",
+              "--steps", "1", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _json_lines(r.stdout)[0]
+    assert res["config"]["preset"] == "baseline4"
+    assert res["config"]["parallelism"].startswith("tp2_pp2_dp1_zero1_ac-every_layer_sp")

@@ -32,6 +32,9 @@ SMALL = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "
         ("8", "2", "1", "1", []),                             # tp2 x dp4 (BASELINE #3 layout)
         ("4", "1", "1", "2", ["--activation-checkpointing", "every_layer"]),
         ("2", "1", "1", "2", ["--lora", "--lora-rank", "8"]),         # LoRA fast path under ZeRO dp2
+        ("8", "2", "1", "1", ["--preset", "baseline3"]),              # BASELINE #3 preset: + SP, 4 comm pieces
+        ("8", "2", "2", "4", ["--preset", "baseline4"]),              # BASELINE #4 preset
+        ("8", "1", "1", "1", ["--preset", "baseline5", "--lora-rank", "8"]),  # BASELINE #5 preset
     ],
 )
 def test_bench_rehearsal_gloo_gpu(layout):
