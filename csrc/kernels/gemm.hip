@@ -202,8 +202,14 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
 #undef SA_RING_READ
 #undef SA_RING_PIECE
     wait_vm<0>();
-    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators
+    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
+    // and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without it hipcc hoists
+    // the first v_accvgpr_reads in among the last MFMAs, which then read stale AGPRs)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
     // epilogue: acc[i][j][e] = C[m0 + 128wm + 16i + (lane & 15)][n0 + 128wn + 16j + 4(lane >> 4) + e]
     const int r = lane & 15, q4 = 4 * (lane >> 4);
