@@ -84,6 +84,14 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// Rotates the pair (x0, x1) by the angle with cosine c and sine s (RoPE).  ONE spelled-out contraction shared by every
+// rotating kernel -- the training RoPE (forward and the transposed backward rotation), the graph-decode RoPE + K/V
+// append step and the GEMV RoPE epilogue -- so all of them round identically whatever hipcc would contract.
+__device__ __forceinline__ void rot_pair(float x0, float x1, float c, float s, float& o0, float& o1) {
+    o0 = __builtin_fmaf(x0, c, -(x1 * s));
+    o1 = __builtin_fmaf(x1, c, x0 * s);
+}
+
 }  // namespace sa
 
 #define SA_CHECK_LAUNCH() (void)hipGetLastError()

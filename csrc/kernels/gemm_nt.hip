@@ -55,7 +55,7 @@ __device__ __forceinline__ void hard_barrier() {
 }
 __device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
 
-template <int EPI>
+template <int EPI, bool SPLIT5>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
                                                          const u16* __restrict__ B, int ldb, uint32_t b_bytes, int M,
                                                          int N, int K, NtEpi ep) {
@@ -103,20 +103,20 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     // piece P (0..15; even: A piece P/2, odd: B piece P/2) of stage U into stage buffer BUF.  Inline asm so the
     // waitcnt pass does not drain the pipeline in front of every ds_read (it cannot tell which LDS bytes a
     // compiler-visible LDS-DMA writes); m0 is written in the statement that reads it.
-#define NT_PIECE(P, BUF, U)                                                                                       \
+#define NT_PIECE_AT(ISB, I, LBASE, U)                                                                             \
     {                                                                                                             \
-        const int i_ = (P) >> 1;                                                                                  \
-        const uint32_t l_ = lds0 + (BUF) * kStage + (((P) & 1) ? kImg : 0) + (wave + 4 * i_) * 1024;             \
+        const uint32_t l_ = (LBASE) + (wave + 4 * (I)) * 1024;                                                    \
         const int ku_ = (U) * 128;                                                                                \
-        if ((P) & 1)                                                                                              \
+        if (ISB)                                                                                                  \
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
-                         "v"(vb), "s"(rsb), "s"(bbase + i_ * bstep + ku_)                                          \
+                         "v"(vb), "s"(rsb), "s"(bbase + (I) * bstep + ku_)                                         \
                          : "m0");                                                                                 \
         else                                                                                                      \
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
-                         "v"(va), "s"(rsa), "s"(abase + i_ * astep + ku_)                                          \
+                         "v"(va), "s"(rsa), "s"(abase + (I) * astep + ku_)                                         \
                          : "m0");                                                                                 \
     }
+#define NT_PIECE(P, BUF, U) NT_PIECE_AT((P) & 1, (P) >> 1, lds0 + (BUF) * kStage + (((P) & 1) ? kImg : 0), U)
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -124,24 +124,27 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+    auto frag = [&](int off, int i) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(smem + off + i * 2048); };
+    const int fr = lane & 15, fg = lane >> 4, ff = fr >> 1;
+    // lane l holds row 16i + (l & 15) of its wave's 128 rows, k chunk 4h + (l >> 4) of the stage; stored chunk
+    // = c ^ f(r), f = ((l & 15) >> 1)
+    const int lo0 = fr * 128 + 16 * (fg ^ ff), lo1 = fr * 128 + 16 * ((fg ^ ff) ^ 4);
+    if constexpr (!SPLIT5) {
+    // ---- two stage buffers [A | B] of 64 KiB.  One opaque VGPR per (buffer, half, operand); fragment i in the
+    // ds_read immediate (i * 2048 + the B image's 32 KiB < 64 KiB).
     // ---- fragments: lane l holds row 16i + (l & 15) of its wave's 128 rows, k chunk 4h + (l >> 4) of the stage;
     // stored chunk = c ^ f(r), f = ((l & 15) >> 1).  One opaque VGPR per (buffer, half, operand); fragment i in the
     // ds_read immediate (i * 2048 + the B image's 32 KiB < 64 KiB).
     int oa[2][2], ob[2][2];
-    {
-        const int r = lane & 15, g = lane >> 4, f = r >> 1;
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int lo = r * 128 + 16 * ((g ^ f) ^ (4 * h));
-                oa[s][h] = s * kStage + wm * 128 * 128 + lo;
-                ob[s][h] = s * kStage + kImg + wn * 128 * 128 + lo;
-                asm volatile("" : "+v"(oa[s][h]), "+v"(ob[s][h]));
-            }
-    }
-    auto frag = [&](int off, int i) -> bf16x8 { return *reinterpret_cast<const bf16x8*>(smem + off + i * 2048); };
-    bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+        for (int h = 0; h < 2; ++h) {
+            oa[s][h] = s * kStage + wm * 128 * 128 + (h ? lo1 : lo0);
+            ob[s][h] = s * kStage + kImg + wn * 128 * 128 + (h ? lo1 : lo0);
+            asm volatile("" : "+v"(oa[s][h]), "+v"(ob[s][h]));
+        }
 
     // sub-step 0 of stage U (buffer BUF): MFMAs on F0, F1 of the same stage read one fragment per 3 MFMAs over the
     // first 48 (retired well before the waits); then own
@@ -202,7 +205,105 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     NT_SUB1(1, u + 1, false, false)
 #undef NT_SUB0
 #undef NT_SUB1
+    } else {
+    // ---- five 32-KiB images: A[0..1] at 0 / 32 KiB, B[0..2] at 64 / 96 / 128 KiB (all 160 KiB of LDS).  Stage s
+    // lives in A[s % 2] and B[s % 3]; B's third buffer lets stage t+2's B image be staged during sub-step (t, 0)
+    // (B[(t+2) % 3] was last read before barrier t-1) and its A image during (t, 1) (A[t % 2] was last read before
+    // barrier t), so every sub-step carries 8 DMA pieces + 16 fragment reads beside its 64 MFMAs instead of one
+    // sub-step carrying all 16 pieces.  End of (t, 0): own reads retired, vmcnt(8) (stage t+1 landed, the 8 B pieces
+    // of stage t+2 just issued stay in flight), barrier t.  The B buffer roles rotate in registers (cur, next,
+    // next-next), the A buffers by the 2-stage unroll.
+    int oa[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        oa[s][0] = s * kImg + wm * 128 * 128 + lo0;
+        oa[s][1] = s * kImg + wm * 128 * 128 + lo1;
+        asm volatile("" : "+v"(oa[s][0]), "+v"(oa[s][1]));
+    }
+    int obc0 = 2 * kImg + wn * 128 * 128 + lo0, obc1 = obc0 - lo0 + lo1;
+    int obn0 = obc0 + kImg, obn1 = obc1 + kImg;
+    int obnn0 = obc0 + 2 * kImg, obnn1 = obc1 + 2 * kImg;
+    uint32_t lbnn = lds0 + 4 * kImg;  // LDS byte address of B[(t+2) % 3]
+    uint32_t lbc = lds0 + 2 * kImg;
+    uint32_t lbn = lds0 + 3 * kImg;
+#define NT5_ROTATE()                                                                                              \
+    {                                                                                                             \
+        const int t0_ = obc0, t1_ = obc1;                                                                         \
+        obc0 = obn0; obc1 = obn1; obn0 = obnn0; obn1 = obnn1; obnn0 = t0_; obnn1 = t1_;                           \
+        const uint32_t tl_ = lbc;                                                                                 \
+        lbc = lbn; lbn = lbnn; lbnn = tl_;                                                                        \
+        asm volatile("" : "+v"(obc0), "+v"(obc1), "+v"(obn0), "+v"(obn1), "+v"(obnn0), "+v"(obnn1));             \
+    }
+    // sub-step (U, 0), A buffer SA: MFMAs on F0, F1 read one fragment per 3 MFMAs over the first 48, stage U+2's
+    // B pieces (PIECES) one per 8 MFMAs; retire own reads + stage U+1, barrier
+#define NT5_SUB0(SA, U, PIECES)                                                                                   \
+    {                                                                                                             \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
+            mfma(acc[i][j], fb0[j], fa0[i]);                                                                      \
+            const int m_ = i * 8 + j;                                                                             \
+            if (m_ % 3 == 1 && m_ < 48) {                                                                         \
+                const int f_ = m_ / 3;                                                                            \
+                if (f_ < 8) fb1[f_] = frag(obc1, f_);                                                             \
+                else fa1[f_ - 8] = frag(oa[SA][1], f_ - 8);                                                       \
+            }                                                                                                     \
+            if ((PIECES) && (m_ & 7) == 7) NT_PIECE_AT(true, m_ >> 3, lbnn, (U) + 2)                            \
+        }                                                                                                         \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                        \
+        if (PIECES) wait_vm<8>();                                                                                 \
+        else wait_vm<0>();                                                                                        \
+        hard_barrier();                                                                                           \
+    }
+    // sub-step (U, 1): MFMAs on F1, F0 of stage U+1 (NEXT) read one per 3 MFMAs over the first 48, stage U+2's A
+    // pieces into A[SA] (PIECES) one per 4 MFMAs over the first 32 (the A image has one sub-step less to land)
+#define NT5_SUB1(SA, U, NEXT, PIECES)                                                                             \
+    {                                                                                                             \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
+            mfma(acc[i][j], fb1[j], fa1[i]);                                                                      \
+            const int m_ = i * 8 + j;                                                                             \
+            if ((NEXT) && m_ % 3 == 1 && m_ < 48) {                                                               \
+                const int f_ = m_ / 3;                                                                            \
+                if (f_ < 8) fb0[f_] = frag(obn0, f_);                                                             \
+                else fa0[f_ - 8] = frag(oa[(SA) ^ 1][0], f_ - 8);                                                 \
+            }                                                                                                     \
+            if ((PIECES) && (m_ & 3) == 3 && m_ < 32) NT_PIECE_AT(false, m_ >> 2, lds0 + (SA) * kImg, (U) + 2)   \
+        }                                                                                                         \
+        NT5_ROTATE()                                                                                              \
+    }
+    // prologue: stages 0 and 1 in flight (A[0] B[0], A[1] B[1]), stage 0 landed, barrier, F0 of stage 0
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        NT_PIECE_AT(false, i, lds0, 0)
+        NT_PIECE_AT(true, i, lds0 + 2 * kImg, 0)
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        NT_PIECE_AT(false, i, lds0 + kImg, 1)
+        NT_PIECE_AT(true, i, lds0 + 3 * kImg, 1)
+    }
+    wait_vm<16>();
+    hard_barrier();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+        if (f < 8) fb0[f] = frag(obc0, f);
+        else fa0[f - 8] = frag(oa[0][0], f - 8);
+    }
+    int u = 0;
+    for (; u < T - 2; u += 2) {  // T even (K % 128 == 0, checked by the dispatcher)
+        NT5_SUB0(0, u, true)
+        NT5_SUB1(0, u, true, true)
+        NT5_SUB0(1, u + 1, true)
+        NT5_SUB1(1, u + 1, true, true)
+    }
+    NT5_SUB0(0, u, false)
+    NT5_SUB1(0, u, true, false)
+    NT5_SUB0(1, u + 1, false)
+    NT5_SUB1(1, u + 1, false, false)
+#undef NT5_SUB0
+#undef NT5_SUB1
+#undef NT5_ROTATE
+    }
 #undef NT_PIECE
+#undef NT_PIECE_AT
     wait_vm<0>();
     // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
     // and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without it hipcc hoists
@@ -280,16 +381,18 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         }
     }
 }
-template __global__ void gemm_nt_kernel<EPI_STORE>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
-                                                   uint32_t, int, int, int, NtEpi);
-template __global__ void gemm_nt_kernel<EPI_SWIGLU>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
-                                                    uint32_t, int, int, int, NtEpi);
-template __global__ void gemm_nt_kernel<EPI_SWIGLU_BWD>(const u16* __restrict__, int, uint32_t, const u16* __restrict__,
-                                                        int, uint32_t, int, int, int, NtEpi);
+#define SA_NT_INST(E, S5)                                                                                      \
+    template __global__ void gemm_nt_kernel<E, S5>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, \
+                                                   int, uint32_t, int, int, int, NtEpi);
+SA_NT_INST(EPI_STORE, false) SA_NT_INST(EPI_SWIGLU, false) SA_NT_INST(EPI_SWIGLU_BWD, false)
+SA_NT_INST(EPI_STORE, true) SA_NT_INST(EPI_SWIGLU, true) SA_NT_INST(EPI_SWIGLU_BWD, true)
+#undef SA_NT_INST
 
 }  // namespace sa_gemm_nt
 
 namespace sa_launch {
+static bool g_nt_split5 = true;
+void gemm_nt_set_split5(bool on) { g_nt_split5 = on; }
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
     return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
            lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
@@ -301,8 +404,12 @@ void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, in
     const int nwg = (int)((M / 256) * (N / 256));
     const uint32_t ab = (uint32_t)(M * lda * 2), bb = (uint32_t)(N * ldb * 2);
 #define SA_NT_LAUNCH(E)                                                                                         \
-    hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab,        \
-                       (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
+    if (g_nt_split5)                                                                                            \
+        hipLaunchKernelGGL((gemm_nt_kernel<E, true>), dim3(nwg), dim3(256), 5 * kImg, st, (const u16*)A,       \
+                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep);              \
+    else                                                                                                        \
+        hipLaunchKernelGGL((gemm_nt_kernel<E, false>), dim3(nwg), dim3(256), kLds, st, (const u16*)A,          \
+                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
     if (epi == EPI_SWIGLU) SA_NT_LAUNCH(EPI_SWIGLU);
     else if (epi == EPI_SWIGLU_BWD) SA_NT_LAUNCH(EPI_SWIGLU_BWD);
     else SA_NT_LAUNCH(EPI_STORE);

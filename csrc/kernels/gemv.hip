@@ -195,8 +195,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int6
             if (h < na.nq + na.nkv) {
                 if (d < na.rd) {
                     const float cs = na.cosb[ps * (na.rd / 2) + d / 2], sn = na.sinb[ps * (na.rd / 2) + d / 2];
-                    o0 = v0 * cs - v1 * sn;
-                    o1 = v1 * cs + v0 * sn;
+                    rot_pair(v0, v1, cs, sn, o0, o1);
                 }
                 dst = h < na.nq ? na.q_out + (int64_t)h * na.hd : na.kc + (ps * na.nkv + (h - na.nq)) * na.hd;
             } else {

@@ -95,8 +95,7 @@ __global__ __launch_bounds__(256) void rope_v8_kernel(const T* __restrict__ x, T
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float sj = sn[j] * a.sign;
-                    o0[j] = x0[j] * cs[j] - x1[j] * sj;
-                    o1[j] = x1[j] * cs[j] + x0[j] * sj;
+                    rot_pair(x0[j], x1[j], cs[j], sj, o0[j], o1[j]);
                 }
                 V8<T>::st(orow + p, o0);
                 V8<T>::st(orow + half + p, o1);
@@ -109,8 +108,7 @@ __global__ __launch_bounds__(256) void rope_v8_kernel(const T* __restrict__ x, T
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float sj = sn[j] * a.sign;
-                    o[2 * j] = v[2 * j] * cs[j] - v[2 * j + 1] * sj;
-                    o[2 * j + 1] = v[2 * j + 1] * cs[j] + v[2 * j] * sj;
+                    rot_pair(v[2 * j], v[2 * j + 1], cs[j], sj, o[2 * j], o[2 * j + 1]);
                 }
                 V8<T>::st(orow + e, o);
             }
@@ -143,8 +141,10 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
             const int i0 = INTERLEAVED ? 2 * p : p;
             const int i1 = INTERLEAVED ? 2 * p + 1 : p + half;
             const float x0 = IO<T>::ld(xr, i0), x1 = IO<T>::ld(xr, i1);
-            IO<T>::st(orow, i0, x0 * c - x1 * s);
-            IO<T>::st(orow, i1, x1 * c + x0 * s);
+            float r0, r1;
+            rot_pair(x0, x1, c, s, r0, r1);
+            IO<T>::st(orow, i0, r0);
+            IO<T>::st(orow, i1, r1);
         } else {
             const int j = a.rd + 2 * (p - half);
             const T v0 = xr[j];
@@ -197,8 +197,7 @@ __global__ __launch_bounds__(256) void rope_kv_append_kernel(const T* __restrict
                 V8<float>::ld(sb + p, sn);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    o0[j] = x0[j] * cs[j] - x1[j] * sn[j];
-                    o1[j] = x1[j] * cs[j] + x0[j] * sn[j];
+                    rot_pair(x0[j], x1[j], cs[j], sn[j], o0[j], o1[j]);
                 }
                 V8<T>::st(orow + p, o0);
                 V8<T>::st(orow + half + p, o1);
@@ -210,8 +209,7 @@ __global__ __launch_bounds__(256) void rope_kv_append_kernel(const T* __restrict
                 const f32x4 sn = *reinterpret_cast<const f32x4*>(sb + e / 2);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    o[2 * j] = v[2 * j] * cs[j] - v[2 * j + 1] * sn[j];
-                    o[2 * j + 1] = v[2 * j + 1] * cs[j] + v[2 * j] * sn[j];
+                    rot_pair(v[2 * j], v[2 * j + 1], cs[j], sn[j], o[2 * j], o[2 * j + 1]);
                 }
                 V8<T>::st(orow + e, o);
             }

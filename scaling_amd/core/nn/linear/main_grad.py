@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from ....ops.attention import stash_gemm
 from ....ops.gemm import linear as gemm_linear
-from ....ops.gemm import transpose2d, wgrad
+from ....ops.gemm import mm_nt, transpose2d, wgrad
 from ...utils.debug_env import side_streams_enabled
 
 _GEN = [0]
@@ -65,7 +65,7 @@ _sync_queued = [-1]  # autograd graph task id whose end-of-backward sync is queu
 
 def wgrad_stream(device: torch.device) -> Optional[Any]:
     """The side stream of this device's GEMM-fused weight-gradient GEMMs (None when disabled / not on a GPU)."""
-    if not _WGRAD_STREAM_ENABLED or device.type != "cuda" or not side_streams_enabled():
+    if not _WGRAD_STREAM_ENABLED or device.type != "cuda" or not side_streams_enabled("wgrad"):
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _wgrad_streams.get(idx)
@@ -175,6 +175,50 @@ def _main_grad_target(weights: Sequence[torch.Tensor]) -> Optional[torch.Tensor]
     return _adjacent([w.grad for w in weights])
 
 
+def weight_grads(g2: torch.Tensor, x2: torch.Tensor, weights: Sequence[torch.Tensor], splits: Sequence[int]
+                 ) -> list[Optional[torch.Tensor]]:
+    """Weight gradients ``dW_i (+)= g2[:, cols_i]^T x2`` of weights sharing the input ``x2``, as ONE GEMM.
+
+    Main-grad weights (all of them attached to the optimizer's flat buffers, stored back to back) get their gradient
+    accumulated in place by the GEMM (beta = 0 on the first write of a lazily zeroed step), the optimizer's bucket-ready
+    callbacks run, and None is returned for each; otherwise the gradients are returned (split per weight).  Row masks
+    (``_sa_grad_row_mask``) are folded into the output-gradient columns first."""
+    n = len(weights)
+    masks = [getattr(wt, "_sa_grad_row_mask", None) for wt in weights]
+    if any(m is not None for m in masks):
+        col = torch.cat([m.reshape(-1).to(g2.device, g2.dtype) if m is not None else g2.new_ones(s)
+                         for m, s in zip(masks, splits)])
+        g2 = g2 * col
+    target = _main_grad_target(weights)
+    if target is None:
+        dw = wgrad(g2, x2)
+        return list(torch.split(dw, list(splits), dim=0)) if n > 1 else [dw]
+    # lazily zeroed gradients (optimizer ``lazy_grad_zeroing``): the first write of the step overwrites (beta = 0)
+    # instead of accumulating into a zeroed buffer
+    fresh = [getattr(wt, "_sa_fresh", False) for wt in weights]
+    accumulate = not all(fresh)
+    for wt, f in zip(weights, fresh):
+        if f:
+            wt._sa_fresh = False
+            if accumulate:
+                wt.grad.zero_()
+    ws = wgrad_stream(g2.device)
+    if ws is not None:
+        ws.wait_stream(torch.cuda.current_stream(g2.device))
+        with torch.cuda.stream(ws):
+            wgrad(g2, x2, target, accumulate=accumulate)
+        g2.record_stream(ws)  # keep the operands' memory until the side stream is done
+        x2.record_stream(ws)
+        _queue_end_of_backward_sync(g2.device)
+    else:
+        wgrad(g2, x2, target, accumulate=accumulate)
+    for wt in weights:
+        cb = getattr(wt, "_sa_grad_ready", None)
+        if cb is not None:
+            cb(wt)
+    return [None] * n
+
+
 class _MultiLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx: Any, x: torch.Tensor, n: int, want_wt: bool, tp_group: Any,  # type: ignore[override]
@@ -203,47 +247,16 @@ class _MultiLinear(torch.autograd.Function):
         dx = None
         work = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(g, w.t()) if ctx.has_wt else torch.matmul(g, w)  # w is W^T [K, N] with the cache
+            if ctx.has_wt:  # w is the cached W^T [K, N]: dX = g (W^T)^T in the forward GEMM layout
+                dx = mm_nt(g.reshape(-1, g.shape[-1]), w).view(*g.shape[:-1], w.shape[0])
+            else:
+                dx = torch.matmul(g, w)
             if ctx.tp_group is not None:  # TP input-gradient all-reduce overlapped with the wgrad GEMM below
                 dx = dx.contiguous()
                 work = dist.all_reduce(dx, group=ctx.tp_group, async_op=True)
         dws: list[Optional[torch.Tensor]] = [None] * n
         if any(ctx.needs_input_grad[4 : 4 + n]):
-            g2 = g.reshape(-1, g.shape[-1])
-            x2 = x.reshape(-1, x.shape[-1])
-            masks = [getattr(wt, "_sa_grad_row_mask", None) for wt in weights]
-            if any(m is not None for m in masks):
-                col = torch.cat([m.reshape(-1).to(g2.device, g2.dtype) if m is not None else g2.new_ones(s)
-                                 for m, s in zip(masks, ctx.splits)])
-                g2 = g2 * col
-            target = _main_grad_target(weights)
-            if target is not None:
-                # lazily zeroed gradients (optimizer ``lazy_grad_zeroing``): the first write of the step overwrites
-                # (beta = 0) instead of accumulating into a zeroed buffer
-                fresh = [getattr(wt, "_sa_fresh", False) for wt in weights]
-                accumulate = not all(fresh)
-                for wt, f in zip(weights, fresh):
-                    if f:
-                        wt._sa_fresh = False
-                        if accumulate:
-                            wt.grad.zero_()
-                ws = wgrad_stream(g2.device)
-                if ws is not None:
-                    ws.wait_stream(torch.cuda.current_stream(g2.device))
-                    with torch.cuda.stream(ws):
-                        wgrad(g2, x2, target, accumulate=accumulate)
-                    g2.record_stream(ws)  # keep the operands' memory until the side stream is done
-                    x2.record_stream(ws)
-                    _queue_end_of_backward_sync(g2.device)
-                else:
-                    wgrad(g2, x2, target, accumulate=accumulate)
-                for wt in weights:
-                    cb = getattr(wt, "_sa_grad_ready", None)
-                    if cb is not None:
-                        cb(wt)
-            else:
-                dw = wgrad(g2, x2)
-                dws = list(torch.split(dw, ctx.splits, dim=0)) if n > 1 else [dw]
+            dws = weight_grads(g.reshape(-1, g.shape[-1]), x.reshape(-1, x.shape[-1]), weights, ctx.splits)
         dbs: list[Optional[torch.Tensor]] = []
         if ctx.has_bias:
             gb = g.reshape(-1, g.shape[-1]).sum(0)

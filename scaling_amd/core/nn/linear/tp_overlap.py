@@ -30,7 +30,7 @@ _streams: dict[int, Any] = {}
 
 
 def _tp_comm_stream(device: torch.device) -> Optional[Any]:
-    if device.type != "cuda" or not side_streams_enabled():
+    if device.type != "cuda" or not side_streams_enabled("tp_comm"):
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _streams.get(idx)

@@ -3,20 +3,28 @@
 ``ParallelSwiGLUMLP`` keeps the reference parameters (``dense_in``, ``siglu_weight``, ``dense_out``)
 but runs ``dense_in``/``siglu_weight`` as one fused GEMM whose ``[..., 2F]`` output feeds the HIP
 SwiGLU kernel directly (and whose backward receives the fused gradient from that kernel).
+
+With the HIP NT GEMM enabled for its shapes (``ops.gemm.nt_enabled``; model-parallel size 1, no biases, outside a
+GEMM-keeping activation-checkpoint region) the whole MLP is ONE autograd node on the NT kernel's fused epilogues
+(``_SwiGLUMLPFused``): the gate/up GEMM writes ``z = [g | u]`` and ``h = silu(g) u`` in one pass, and the backward's
+down-projection input gradient consumes ``dh`` in registers and writes ``dz`` directly -- no SwiGLU pass over HBM in
+either direction.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Any, Callable, Optional
 
 import torch
 
 from ...ops import swiglu as swiglu_ops
 from ...ops._ext import ext, use_native
+from ...ops.attention import stash_active
+from ...ops.gemm import mm_nt, nt_enabled, transpose2d
 from ..topology import Topology
 from .activation_function import ActivationFunction, get_activation_function
 from .linear import ColumnParallelLinear, RowParallelLinear
 from .linear.fused import fused_column_linear
-from .linear.main_grad import adjacent_weights
+from .linear.main_grad import _transposed, adjacent_weights, weight_grads
 
 
 def _intermediate(io_features: int, factor: float) -> int:
@@ -56,6 +64,49 @@ class ParallelMLP(torch.nn.Module):
         if self.topology is not None and self.topology.config.sequence_parallel:
             return self.dense_out.forward_sequence_parallel(h)
         return self.dense_out(h)
+
+
+class _SwiGLUMLPFused(torch.autograd.Function):
+    """``y = (silu(x Wg^T) * (x Wu^T)) Wd^T`` (TP 1, bias-free) on the NT GEMM kernel's SwiGLU epilogues.
+
+    Forward: one gate/up GEMM writing z and h, one down-projection GEMM.  Saved: x, z, h and the cached transposes
+    (the same activations the unfused MLP keeps).  Backward: ``dz`` straight from the down-projection input-gradient
+    GEMM (SwiGLU backward in its epilogue), weight gradients through ``weight_grads`` (GEMM-accumulated main grads),
+    ``dx = dz Wgu`` on the cached ``Wgu^T``."""
+
+    @staticmethod
+    def forward(ctx: Any, x: torch.Tensor, wg: torch.Tensor, wu: torch.Tensor, wd: torch.Tensor) -> torch.Tensor:  # type: ignore[override]
+        wgu = adjacent_weights([wg, wu])
+        assert wgu is not None
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H)
+        T, F = x2.shape[0], wg.shape[0]
+        z = torch.empty(T, 2 * F, device=x.device, dtype=x.dtype)
+        h = torch.empty(T, F, device=x.device, dtype=x.dtype)
+        ext().gemm_nt_swiglu(x2, wgu, z, h)
+        y = mm_nt(h, wd)
+        wgut = _transposed([wg, wu], wgu)
+        wdt = _transposed([wd], wd)
+        if wgut is None:  # transpose cache disabled (SCALING_AMD_DGRAD_WT=0): per-call transposes
+            wgut = transpose2d(wgu.detach())
+        if wdt is None:
+            wdt = transpose2d(wd.detach())
+        ctx.save_for_backward(x2, z, h, wgut, wdt, wg, wu, wd)
+        ctx.lead = x.shape[:-1]
+        return y.view(*x.shape[:-1], wd.shape[0])
+
+    @staticmethod
+    def backward(ctx: Any, dy: torch.Tensor):  # type: ignore[override]
+        x2, z, h, wgut, wdt, wg, wu, wd = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dz = torch.empty_like(z)
+        ext().gemm_nt_swiglu_bwd(dy2, wdt, z, dz)
+        dwd = weight_grads(dy2, h, [wd], [wd.shape[0]])[0] if ctx.needs_input_grad[3] else None
+        dx = mm_nt(dz, wgut).view(*ctx.lead, x2.shape[1]) if ctx.needs_input_grad[0] else None
+        dwg = dwu = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dwg, dwu = weight_grads(dz, x2, [wg, wu], [wg.shape[0], wu.shape[0]])
+        return dx, dwg, dwu, dwd
 
 
 class ParallelSwiGLUMLP(torch.nn.Module):
@@ -135,7 +186,26 @@ class ParallelSwiGLUMLP(torch.nn.Module):
         s, a = ext().gemv_norm(h2, residual.reshape(rows, -1), nw[0], nw[1], ws[0], 2)
         return ext().gemv_residual(a, ws[1], s).view(residual.shape)
 
+    def _fused_eligible(self, x: torch.Tensor) -> bool:
+        """The one-node MLP on the NT kernel's SwiGLU epilogues applies: GPU bf16, TP 1, bias-free, adjacent gate/up
+        weights, shapes the kernel tiles and the dispatch policy enables, no GEMM-keeping checkpoint region."""
+        if not (use_native(x) and x.dtype == torch.bfloat16 and torch.is_grad_enabled()):
+            return False
+        if self.topology is not None and self.topology.config.model_parallel_size > 1:
+            return False
+        if any(getattr(m, "bias_param", None) is not None for m in (self.dense_in, self.siglu_weight, self.dense_out)):
+            return False
+        if stash_active():
+            return False
+        wgu = adjacent_weights([self.dense_in.weight, self.siglu_weight.weight])
+        x2 = x.reshape(-1, x.shape[-1])
+        return (wgu is not None and nt_enabled(x2, wgu) and bool(ext().gemm_nt_swiglu_ok(x2, wgu))
+                and self.dense_out.weight.shape[1] % 256 == 0 and x.shape[-1] % 256 == 0)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self._fused_eligible(x):
+            return _SwiGLUMLPFused.apply(x.contiguous(), self.dense_in.weight, self.siglu_weight.weight,
+                                         self.dense_out.weight)
         z = fused_column_linear(x, [self.dense_in, self.siglu_weight], self.topology)
         h = swiglu_ops.swiglu_fused(z)
         if self.topology is not None and self.topology.config.sequence_parallel:

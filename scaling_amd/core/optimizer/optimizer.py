@@ -73,7 +73,7 @@ class Optimizer(BaseOptimizer):
         self.dp = topology.config.data_parallel_size
         self._gpu = topology.device.type == "cuda"
         self._comm_stream = (torch.cuda.Stream(device=topology.device)
-                             if (self._gpu and self.dp > 1 and side_streams_enabled()) else None)
+                             if (self._gpu and self.dp > 1 and side_streams_enabled("dp_comm")) else None)
         max_bucket = max(g.bucket_size for g in parameter_groups)
         self._scratch = (
             torch.empty(max_bucket, dtype=torch.float32, device=topology.device)
@@ -281,7 +281,7 @@ class Optimizer(BaseOptimizer):
 
     # ------------------------------------------------------------------ overlapped optimizer step
     def _async_step(self) -> bool:
-        return bool(self._gpu and self.config.overlap_optimizer_step and side_streams_enabled())
+        return bool(self._gpu and self.config.overlap_optimizer_step and side_streams_enabled("opt_step"))
 
     def _step_stream(self) -> Any:
         if self._comm_stream is not None:  # AdamW then the ZeRO all-gather of the bucket, in order, on one stream

@@ -49,8 +49,26 @@ def comm_delay_us() -> int:
         return 0
 
 
-def side_streams_enabled() -> bool:
-    return os.environ.get("SCALING_AMD_SINGLE_STREAM", "0") in ("", "0")
+SIDE_STREAM_FEATURES = ("dp_comm", "opt_step", "wgrad", "tp_comm")
+
+
+def side_streams_enabled(feature: str = "") -> bool:
+    """Whether side-stream ``feature`` runs on its own stream.  ``SCALING_AMD_SINGLE_STREAM`` = 1 folds every side
+    stream onto the compute stream; a comma-separated subset of ``SIDE_STREAM_FEATURES`` folds only those (the race
+    check bisects a multi- vs single-stream difference this way):
+      dp_comm   the data-parallel gradient reduce-scatter / parameter all-gather stream (optimizer)
+      opt_step  the overlapped optimizer update (its own stream when there is no DP stream)
+      wgrad     the weight-gradient GEMM stream (SCALING_AMD_WGRAD_STREAM=1)
+      tp_comm   the tensor-parallel collective stream of the chunked row-parallel GEMMs"""
+    v = os.environ.get("SCALING_AMD_SINGLE_STREAM", "0").strip()
+    if v in ("", "0"):
+        return True
+    if v in ("1", "all"):
+        return False
+    folded = {f.strip() for f in v.split(",")}
+    unknown = folded - set(SIDE_STREAM_FEATURES)
+    assert not unknown, f"SCALING_AMD_SINGLE_STREAM: unknown features {sorted(unknown)} (known: {SIDE_STREAM_FEATURES})"
+    return feature not in folded
 
 
 def debug_env(collectives: bool = False, hip_launch_blocking: bool = False, single_stream: bool = False

@@ -147,6 +147,12 @@ def attention_stash(stash: Optional[AttentionStash], mode: str) -> Iterator[None
         _stash_state.cur = prev
 
 
+def stash_active() -> bool:
+    """Whether a GEMM-keeping checkpoint region (``every_layer_save_matmuls``) is recording or replaying."""
+    cur = getattr(_stash_state, "cur", None)
+    return cur is not None and bool(cur[0].keep_gemms)
+
+
 def stash_gemm(compute: Callable[[], torch.Tensor]) -> torch.Tensor:
     """A linear layer's GEMM output through the checkpoint stash (``every_layer_save_matmuls``): the region's first
     forward records ``compute()``'s output, the recompute in the backward returns it instead of running the GEMM again

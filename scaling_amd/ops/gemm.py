@@ -1,4 +1,6 @@
-"""Weight-gradient GEMM ``dW (+)= dY^T X`` on the hand-written gfx950 kernel (``csrc/kernels/gemm.hip``).
+"""Linear-layer GEMMs on the hand-written gfx950 kernels.
+
+``wgrad``: the weight gradient ``dW (+)= dY^T X`` (``csrc/kernels/gemm.hip``).
 
 Both operands arrive token-major (``dY: [T, N]``, ``X: [T, K]``), i.e. k-strided for this product; the
 kernel stages them as they lie (LDS-DMA) and builds MFMA fragments with the transposing LDS read, in a
@@ -6,11 +8,16 @@ ping-pong schedule.  At the 7B layer shapes it runs 1.05-1.25 PF vs hipBLASLt's 
 (``profiles/gemm_wgrad_r1.log``).  Shapes it does not tile (M/N not multiples of 256, T not a multiple
 of 64) use ``torch.matmul`` / ``addmm_`` (hipBLASLt).
 
-``linear`` is the forward ``x W^T (+ b)`` of every linear layer: at most 4 token rows (token-by-token decoding)
-run the weight-streaming GEMV kernel (``csrc/kernels/gemv.hip``), everything else hipBLASLt.
+``linear`` is the forward ``x W^T (+ b)`` of every linear layer and ``mm_nt`` the input gradient ``dY (W^T)^T`` on
+the cached transpose: at most 4 token rows (token-by-token decoding) run the weight-streaming GEMV kernel
+(``csrc/kernels/gemv.hip``); larger products run the HIP NT kernel (``csrc/kernels/gemm_nt.hip``) where
+``nt_enabled`` says so, else hipBLASLt.  ``SCALING_AMD_NT_GEMM``: ``1`` = the HIP kernel for every shape it tiles,
+``0`` = hipBLASLt everywhere, ``auto`` (default) = the HIP kernel for the (N, K) shapes in ``NT_FASTER`` (measured
+faster than hipBLASLt's tuned solution on MI355X, ``tools/gemm_nt_bench.py``).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -41,6 +48,28 @@ def transpose2d(x: torch.Tensor) -> torch.Tensor:
 
 GEMV_MAX_ROWS = 4
 
+_NT_MODE = os.environ.get("SCALING_AMD_NT_GEMM", "auto")
+# (N out, K in) shapes of y = x W^T where the HIP NT kernel beat hipBLASLt (tools/gemm_nt_bench.py, MI355X)
+NT_FASTER: set[tuple[int, int]] = set()
+
+
+def nt_enabled(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Whether ``a @ b^T`` (2-D, b = [N, K]) runs on the HIP NT kernel (policy above + the kernel's tiling)."""
+    if _NT_MODE == "0" or not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2):
+        return False
+    if _NT_MODE != "1" and (int(b.shape[0]), int(b.shape[1])) not in NT_FASTER:
+        return False
+    return bool(ext().gemm_nt_ok(a, b))
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b^T`` for 2-D ``a`` [M, K] and ``b`` [N, K] (no autograd graph): HIP NT kernel or hipBLASLt."""
+    if nt_enabled(a, b):
+        out = torch.empty(a.shape[0], b.shape[0], device=a.device, dtype=a.dtype)
+        ext().gemm_nt(a, b, out)
+        return out
+    return torch.matmul(a, b.t())
+
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``F.linear(x, w, b)``; decode-sized inputs (<= 4 rows) on the GEMV kernel.
@@ -54,4 +83,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
         x2 = x.reshape(rows, K)
         if ext().gemv_ok(x2, w) and (b is None or b.dtype == w.dtype):
             return ext().gemv(x2, w, b).reshape(*x.shape[:-1], w.shape[0])
+    if b is None and not needs_graph and rows > GEMV_MAX_ROWS and w.dim() == 2 and use_native(x):
+        x2 = x.reshape(rows, K)
+        if nt_enabled(x2, w):
+            return mm_nt(x2, w).reshape(*x.shape[:-1], w.shape[0])
     return torch.nn.functional.linear(x, w, b)

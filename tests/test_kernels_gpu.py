@@ -943,3 +943,39 @@ def test_rope_kv_append_bit_identical(interleaved, rot_frac):
     q = ext().rope_kv_append(qkv, cos, sin, pos, nq, nkv, rd, interleaved, kc, vc)
     assert q is not None
     assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+
+
+@pytest.mark.parametrize("T,H,F", [(512, 256, 512), (1024, 512, 768)])
+def test_swiglu_mlp_fused_node_matches_unfused(T, H, F, monkeypatch):
+    """ParallelSwiGLUMLP as ONE autograd node on the NT GEMM's SwiGLU epilogues (SCALING_AMD_NT_GEMM=1) gives the
+    output, input gradient and weight gradients of the unfused path (hipBLASLt GEMMs + SwiGLU kernels) to bf16
+    accuracy, and both match an fp32 reference."""
+    from scaling_amd.core.nn.mlp import ParallelSwiGLUMLP
+    from scaling_amd.ops import gemm as gemm_ops
+
+    torch.manual_seed(3)
+    mlp = ParallelSwiGLUMLP(H, F / H, bias=False, device=torch.device(DEV), dtype=torch.bfloat16)
+    x = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(gemm_ops, "_NT_MODE", mode)
+        assert mlp._fused_eligible(x) == (mode == "1")
+        for p in mlp.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = mlp(xi)
+        y.backward(dy)
+        res[mode] = [y.float(), xi.grad.float()] + [p.grad.float() for p in (mlp.dense_in.weight,
+                                                                              mlp.siglu_weight.weight,
+                                                                              mlp.dense_out.weight)]
+    xf = x.float().reshape(-1, H).requires_grad_(True)
+    wg, wu, wd = (p.detach().float().requires_grad_(True) for p in (mlp.dense_in.weight, mlp.siglu_weight.weight,
+                                                                   mlp.dense_out.weight))
+    yf = (torch.nn.functional.silu(xf @ wg.t()) * (xf @ wu.t())) @ wd.t()
+    yf.backward(dy.float().reshape(-1, H))
+    ref = [yf, xf.grad, wg.grad, wu.grad, wd.grad]
+    for a, b, r in zip(res["1"], res["0"], ref):
+        scale = r.abs().max().item()
+        assert (a.reshape(r.shape) - r).abs().max().item() < 0.03 * scale
+        assert (a - b).abs().max().item() < 0.03 * scale

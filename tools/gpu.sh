@@ -11,6 +11,7 @@
 #   attn       tools/attn_only.py (isolated attention at the 7B shape)
 #   decode     tools/decode_bench.py
 #   race       the multi- vs single-stream race check (tests/test_gpu_rehearsal.py -k race_check)
+#   race_bisect  tools/race_bisect.py: which side stream makes a layout differ from its single-stream twin
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -49,6 +50,8 @@ for step in "$@"; do
     race)
         $T 600 $PY -m pytest tests/test_gpu_rehearsal.py -m gpu -x -v --timeout 300 --timeout-method thread \
             -k "race_check" > gpurun_out/race_$TAG.log 2>&1 ;;
+    race_bisect)
+        $T 900 $PY tools/race_bisect.py ${RACE_ARGS:-} > gpurun_out/race_bisect_$TAG.log 2>&1 ;;
     *)
         echo "unknown step $step"; exit 2 ;;
     esac
