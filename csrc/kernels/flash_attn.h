@@ -143,48 +143,6 @@ __device__ __forceinline__ void dma_load(const DmaTile<D, W, R>& t, const void* 
     t.load(base, tok, rows, tile, wave_u);
 }
 
-// LDS-DMA of a [64][D] tile as inline asm: invisible to the compiler's waitcnt pass, which otherwise puts a
-// vmcnt(0) in front of the next LDS read of ANY buffer and so waits for the tile just issued; the caller retires
-// the pieces with its own s_waitcnt vmcnt before the barrier that publishes them.  m0 is saved / restored around
-// each piece (compiler-reserved), and the descriptor may be fresh from v_readfirstlane: s_nop 4 opens the string.
-template <int D, int W, int R>
-__device__ __forceinline__ void dma_tile_asm(const DmaTile<D, W, R>& t, const void* base, int64_t tok, int rows, char* tile,
-                                             int wave_u) {
-    typedef int i32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t ad = reinterpret_cast<uint64_t>(base);
-    const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)ad),
-                      (int)(__builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32)) & 0xffff),
-                      (int)__builtin_amdgcn_readfirstlane((uint32_t)max(rows, 0) * (uint32_t)tok * 2u), kBufFlags};
-#pragma unroll
-    for (int i = 0; i < DmaTile<D, W, R>::NPW; ++i) {
-        if (!(DmaTile<D, W, R>::PIECES >= W || wave_u + W * i < DmaTile<D, W, R>::PIECES)) continue;  // wave-uniform
-        const uint32_t lds = __builtin_amdgcn_readfirstlane(
-            (uint32_t)reinterpret_cast<uintptr_t>((lds_void*)(tile + (wave_u + W * i) * 1024)));
-        int keep;
-        asm volatile(
-            "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(lds), "v"(t.voff[i]), "s"(rs));
-    }
-}
-
-// one dword per lane (256 B) by LDS-DMA into lds (wave-uniform byte address), same conventions as dma_tile_asm
-__device__ __forceinline__ void dma_dword_asm(const void* base, uint32_t nbytes, int voff, char* lds_dst) {
-    typedef int i32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t ad = reinterpret_cast<uint64_t>(base);
-    const i32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)ad),
-                      (int)(__builtin_amdgcn_readfirstlane((uint32_t)(ad >> 32)) & 0xffff),
-                      (int)__builtin_amdgcn_readfirstlane(nbytes), kBufFlags};
-    const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)lds_dst));
-    int keep;
-    asm volatile(
-        "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-        "buffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(lds), "v"(voff), "s"(rs));
-}
-
 // 3-way max without the canonicalising v_max the compiler wraps around fmaxf
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
     float r;

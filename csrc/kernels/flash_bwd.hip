@@ -89,14 +89,11 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
 //   S = Q K^T, dP = dO V^T (row reads), p = exp2(S c - lse2), dS = p (dP - delta),
 //   dV^T += dO^T P, dK^T += Q^T dS (transposed reads; P / dS accumulators are the B operands).
 // Query rows past the segment arrive as zeros (Q = dO = 0, lse2 = delta = 0) and contribute nothing.
-// OCC: waves per SIMD the register budget is sized for (1: the whole register file, with explicit read-ahead);
-// ADMA: the per-tile LDS-DMA as inline asm retired by an explicit vmcnt(0) before the barrier (compiler-visible
-// LDS-DMA makes hipcc wait for the NEXT tile's DMA in front of this tile's transposed LDS reads).
-// PAIR (with OCC 1 and ADMA, no dropout): two query tiles per barrier, software-pipelined inside the wave: the S/dP
-// MFMAs of tile B run beside tile A's exp / dS VALU and tile A's dV/dK MFMAs beside tile B's (one wave per SIMD
-// issues its VALU in the MFMA gaps); boundary (masked) pairs take the sequential tile path.  Four LDS buffers.
-template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false, bool PAIR = false>
-__global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
+// Variants measured against this one and dropped (one wave per SIMD with explicit read-ahead, inline-asm LDS-DMA,
+// paired software-pipelined query tiles): profiles/attn_bwd_variants_ab_r3.log, attn_bwd_pair_ab_r3.log; their code is
+// in git history before commit "Delete losing attention variants".
+template <int D, bool F16, bool DROP>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int QT = 32, TILE = QT * D * 2, BUF = 2 * TILE + 512, VIMG = 128 * D * 2, NKS = D / 16, NT = D / 32;
@@ -153,24 +150,13 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
     // incrementally (no runtime divisions in the loop)
     auto issue = [&](int gi, int qi, char* buf) {
         const int qt = qlo + qi * QT, hq = h0 + gi;
-        if constexpr (ADMA) {
-            dma_tile_asm(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
-            dma_tile_asm(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE,
-                         wave);
-        } else {
-            dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
-            dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
-        }
+        dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
+        dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
         if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
             const int64_t ix = (int64_t)hq * a.lse_stride + q0s + qt;
             const uint32_t nb = (uint32_t)max(min(QT, Lq - qt), 0) * 4u;
-            if constexpr (ADMA) {
-                dma_dword_asm(a.lse2 + ix, nb, 4 * lane, buf + 2 * TILE);
-                dma_dword_asm(a.delta + ix, nb, 4 * lane, buf + 2 * TILE + 256);
-            } else {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
-            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.lse2 + ix, nb), (lds_void*)(buf + 2 * TILE), 4, 4 * lane, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(uniform_rsrc(a.delta + ix, nb), (lds_void*)(buf + 2 * TILE + 256), 4, 4 * lane, 0, 0, 0);
         }
     };
     f32x16 dk[NT], dv[NT];
@@ -189,31 +175,7 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
                                (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
         f32x16 s = f32x16{}, dp = f32x16{};
-        if constexpr (OCC == 1) {
-            // one wave per SIMD: the register file has room to read PD k-steps ahead, so no MFMA waits on the LDS
-            // latency of its own operands
-            constexpr int PD = 3;
-            bf16x8 rq[PD], rdo[PD], rv[PD];
-#pragma unroll
-            for (int ks = 0; ks < PD; ++ks) {
-                rq[ks] = rd_row<D>(Q, 0, lo.row(ks));
-                rdo[ks] = rd_row<D>(DO, 0, lo.row(ks));
-                rv[ks] = rd_row<D>(vw_img, 0, lo.row(ks));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const int b = ks % PD;
-                s = mma<F16>(rq[b], kf[ks], s);
-                dp = mma<F16>(rdo[b], rv[b], dp);
-                if (ks + PD < NKS) {
-                    rq[b] = rd_row<D>(Q, 0, lo.row(ks + PD));
-                    rdo[b] = rd_row<D>(DO, 0, lo.row(ks + PD));
-                    rv[b] = rd_row<D>(vw_img, 0, lo.row(ks + PD));
-                }
-                __builtin_amdgcn_sched_barrier(0);  // keep the read-ahead: the scheduler would sink reads to their use
-            }
-        } else {
+        {
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 s = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], s);
@@ -263,30 +225,7 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 }
             }
         }
-        if constexpr (OCC == 1) {
-            const bf16x8 pb[2] = {pack_acc_t<F16>(s, 0), pack_acc_t<F16>(s, 1)};
-            const bf16x8 db[2] = {pack_acc_t<F16>(dp, 0), pack_acc_t<F16>(dp, 1)};
-            constexpr int NS = 2 * NT, PD = 3;  // steps (ss, t); fragments PD steps ahead
-            bf16x8 fo[PD], fq[PD];
-#pragma unroll
-            for (int i = 0; i < PD; ++i) {
-                fo[i] = rd_tr<D>(DO, 16 * (i / NT) * D * 2, lo, i % NT);
-                fq[i] = rd_tr<D>(Q, 16 * (i / NT) * D * 2, lo, i % NT);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                const int ss = i / NT, t = i % NT, b = i % PD;
-                dv[t] = mma<F16>(fo[b], pb[ss], dv[t]);
-                dk[t] = mma<F16>(fq[b], db[ss], dk[t]);
-                if (i + PD < NS) {
-                    const int j = i + PD;
-                    fo[b] = rd_tr<D>(DO, 16 * (j / NT) * D * 2, lo, j % NT);
-                    fq[b] = rd_tr<D>(Q, 16 * (j / NT) * D * 2, lo, j % NT);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
+        {
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 const bf16x8 pb = pack_acc_t<F16>(s, ss), db = pack_acc_t<F16>(dp, ss);
@@ -314,132 +253,10 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
             ++g;
         }
     };
-    if constexpr (PAIR && OCC == 1 && ADMA && !DROP) {
-        static_assert(PAIR ? true : true, "");
-        // ---- paired, software-pipelined path (see the template comment)
-        auto sdp = [&](const char* Q, f32x16& sx, f32x16& dpx) {
-            const char* DO = Q + TILE;
-            sx = f32x16{};
-            dpx = f32x16{};
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                sx = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], sx);
-                dpx = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dpx);
-            }
-        };
-        auto soft = [&](const char* Q, f32x16& sx, f32x16& dpx, bf16x8 (&pb)[2], bf16x8 (&db)[2]) {
-            const float* LS = reinterpret_cast<const float*>(Q + 2 * TILE);
-            const float* DL = LS + 64;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 l4 = *reinterpret_cast<const f32x4*>(LS + 8 * g + 4 * h);
-                const f32x4 d4 = *reinterpret_cast<const f32x4*>(DL + 8 * g + 4 * h);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float pr = fast_exp2(__builtin_fmaf(sx[4 * g + j], c2, -l4[j]));
-                    sx[4 * g + j] = pr;
-                    dpx[4 * g + j] = pr * (dpx[4 * g + j] - d4[j]);
-                }
-            }
-            pb[0] = pack_acc_t<F16>(sx, 0);
-            pb[1] = pack_acc_t<F16>(sx, 1);
-            db[0] = pack_acc_t<F16>(dpx, 0);
-            db[1] = pack_acc_t<F16>(dpx, 1);
-        };
-        auto dvdk = [&](const char* Q, const bf16x8 (&pb)[2], const bf16x8 (&db)[2]) {
-            const char* DO = Q + TILE;
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    dv[t] = mma<F16>(rd_tr<D>(DO, 16 * ss * D * 2, lo, t), pb[ss], dv[t]);
-                    dk[t] = mma<F16>(rd_tr<D>(Q, 16 * ss * D * 2, lo, t), db[ss], dk[t]);
-                }
-        };
-        auto masked = [&](int gi, int qi) {
-            const int qt = qlo + qi * QT;
-            const int win = (h0 + gi) < a.local_heads ? a.window : -1;
-            return (a.causal && kw0 + 31 > qt + off) ||
-                   (win >= 0 && (kw0 < qt + QT - 1 + off - win || (!a.causal && kw0 + 31 > qt + off + win)));
-        };
-        auto pair = [&](const char* QA, const char* QB) {
-            f32x16 sA, dpA, sB, dpB;
-            bf16x8 pbA[2], dbA[2], pbB[2], dbB[2];
-            sdp(QA, sA, dpA);
-#pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            sdp(QB, sB, dpB);
-            soft(QA, sA, dpA, pbA, dbA);
-#pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            dvdk(QA, pbA, dbA);
-            soft(QB, sB, dpB, pbB, dbB);
-#pragma unroll
-            for (int i = 0; i < 4 * NT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 2);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            dvdk(QB, pbB, dbB);
-#pragma unroll
-            for (int i = 0; i < 4 * NT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 3);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 3);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        // (an array of buffer pointers would lose the LDS address space: every read turned into a flat address)
-        auto bufs = [&](int k) { return smem + VIMG + (k & 3) * BUF; };
-        if (nwork > 0) {
-            issue(ig, iq, bufs(0));
-            adv(ig, iq);
-        }
-        if (nwork > 1) {
-            issue(ig, iq, bufs(1));
-            adv(ig, iq);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int w = 0;
-        for (; w + 1 < nwork; w += 2) {
-            if (w + 2 < nwork) {
-                issue(ig, iq, bufs(w + 2));
-                adv(ig, iq);
-            }
-            if (w + 3 < nwork) {
-                issue(ig, iq, bufs(w + 3));
-                adv(ig, iq);
-            }
-            const int gA = cg, qA = cq;
-            adv(cg, cq);
-            const int gB = cg, qB = cq;
-            adv(cg, cq);
-            if (!masked(gA, qA) && !masked(gB, qB)) {
-                pair(bufs(w), bufs(w + 1));
-            } else {
-                tile(bufs(w), gA, qA);
-                tile(bufs(w + 1), gB, qB);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-        if (w < nwork) tile(bufs(w), cg, cq);
-    } else {
     if (nwork > 0) {
         issue(ig, iq, buf0);
         adv(ig, iq);
     }
-    if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int w = 0;
     for (; w + 1 < nwork; w += 2) {
@@ -447,7 +264,6 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
         adv(ig, iq);
         tile(buf0, cg, cq);
         adv(cg, cq);
-        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (w + 2 < nwork) {
             issue(ig, iq, buf0);
@@ -455,11 +271,9 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
         }
         tile(buf1, cg, cq);
         adv(cg, cq);
-        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     if (w < nwork) tile(buf0, cg, cq);
-    }
 
     if (mykey < Lk) {
         if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel
@@ -503,9 +317,8 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dkdv_kernel(BwdArgs a) {
 // dQ: workgroup = 4 waves x 32 queries of one (segment, q head); query on the lane (Q, dO rows are
 // register-resident B operands), K / V tiles of 64 keys double-buffered in LDS by LDS-DMA.  Per 32-key block:
 //   S^T = K Q^T, dP^T = V dO^T, p = exp2(S c - lse2), dS = p (dP - delta), dQ^T += K^T dS^T.
-// RA: explicit LDS read-ahead pinned by sched barriers (hipcc sinks each read right in front of its MFMA)
-template <int D, bool F16, bool DROP, int OCC = 2, bool ADMA = false, bool RA = false>
-__global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
+template <int D, bool F16, bool DROP>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
@@ -560,13 +373,8 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
     //  hipcc's host pass treat the kernel as undefined and drop its launch stub)
 #define SA_DQ_ISSUE(KT, BUFP)                                                                          \
     do {                                                                                               \
-        if constexpr (ADMA) {                                                                          \
-            dma_tile_asm(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);        \
-            dma_tile_asm(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u); \
-        } else {                                                                                       \
-            dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);            \
-            dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u);     \
-        }                                                                                              \
+        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);                \
+        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u);         \
     } while (0)
     f32x16 dq[NT];
 #pragma unroll
@@ -580,26 +388,7 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             f32x16 s = f32x16{}, dp = f32x16{};
-            if constexpr (RA) {
-                constexpr int PD = 2;
-                bf16x8 rk[PD], rv[PD];
-#pragma unroll
-                for (int ks = 0; ks < PD; ++ks) {
-                    rk[ks] = rd_row<D>(K, 32 * b * D * 2, lo.row(ks));
-                    rv[ks] = rd_row<D>(V, 32 * b * D * 2, lo.row(ks));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    s = mma<F16>(rk[ks % PD], qf[ks], s);
-                    dp = mma<F16>(rv[ks % PD], df[ks], dp);
-                    if (ks + PD < NKS) {
-                        rk[ks % PD] = rd_row<D>(K, 32 * b * D * 2, lo.row(ks + PD));
-                        rv[ks % PD] = rd_row<D>(V, 32 * b * D * 2, lo.row(ks + PD));
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            } else {
+            {
 #pragma unroll
                 for (int ks = 0; ks < NKS; ++ks) {
                     s = mma<F16>(rd_row<D>(K, 32 * b * D * 2, lo.row(ks)), qf[ks], s);
@@ -629,23 +418,7 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
                     dp[r] = p * (dp[r] - dlt);
                 }
             }
-            if constexpr (RA) {
-                const bf16x8 dbs[2] = {pack_acc_t<F16>(dp, 0), pack_acc_t<F16>(dp, 1)};
-                constexpr int NS = 2 * NT, PD = 2;  // step i = (ss = i / NT, t = i % NT)
-                bf16x8 fk[PD];
-#pragma unroll
-                for (int i = 0; i < PD; ++i) fk[i] = rd_tr<D>(K, (32 * b + 16 * (i / NT)) * D * 2, lo, i % NT);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    dq[i % NT] = mma<F16>(fk[i % PD], dbs[i / NT], dq[i % NT]);
-                    if (i + PD < NS) {
-                        const int j = i + PD;
-                        fk[i % PD] = rd_tr<D>(K, (32 * b + 16 * (j / NT)) * D * 2, lo, j % NT);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            } else {
+            {
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
                     const bf16x8 db = pack_acc_t<F16>(dp, ss);
@@ -660,18 +433,15 @@ __global__ __launch_bounds__(256, OCC) void fa_bwd_dq_kernel(BwdArgs a) {
     char* buf0 = smem;
     char* buf1 = smem + 2 * TILE;
     if (klo < khi) SA_DQ_ISSUE(klo, buf0);
-    if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int ntiles = khi > klo ? (khi - klo + 63) / 64 : 0;
     int kt = klo;
     for (int pr = 0; pr < ntiles / 2; ++pr, kt += 128) {
         SA_DQ_ISSUE(kt + 64, buf1);
         tile(buf0, kt);
-        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (kt + 128 < khi) SA_DQ_ISSUE(kt + 128, buf0);
         tile(buf1, kt + 64);
-        if constexpr (ADMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     if (ntiles & 1) tile(buf0, kt);
@@ -719,59 +489,19 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
-// A/B switches (read once): SCALING_AMD_FA_BWD_OCC=1 -> one wave per SIMD with read-ahead; SCALING_AMD_FA_BWD_ADMA=1 ->
-// per-tile LDS-DMA as inline asm with its own vmcnt
-static int bwd_occ() {
-    static const int v = [] {
-        const char* e = getenv("SCALING_AMD_FA_BWD_OCC");
-        return e && atoi(e) == 1 ? 1 : 2;
-    }();
-    return v;
-}
-static bool bwd_pair() {  // SCALING_AMD_FA_BWD_PAIR=1: paired, software-pipelined dK/dV (D = 128, no dropout)
-    static const bool v = [] {
-        const char* e = getenv("SCALING_AMD_FA_BWD_PAIR");
-        return e && atoi(e) == 1;
-    }();
-    return v;
-}
-static bool bwd_adma() {
-    static const bool v = [] {
-        const char* e = getenv("SCALING_AMD_FA_BWD_ADMA");
-        return e && atoi(e) == 1;
-    }();
-    return v;
-}
-
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
-        if (D == 128 && bwd_pair() && !DROP)
-            hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1, true, true>), grid, 256,
-                               128 * D * 2 + 4 * (2 * 32 * D * 2 + 512), st, a);
-        else if (D == 128 && bwd_occ() == 1 && bwd_adma())
-            hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
-        else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
-        else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);
-        else if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     {
         dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
-        static const bool ra = [] {
-            const char* e = getenv("SCALING_AMD_FA_BWD_RA");
-            return e && atoi(e) == 1;
-        }();
-        if (D == 128 && ra) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 2, false, true>), grid, 256, lds, st, a);
-        else if (D == 128 && bwd_occ() == 1 && bwd_adma())
-            hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1, true>), grid, 256, lds, st, a);
-        else if (D == 128 && bwd_occ() == 1) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 1>), grid, 256, lds, st, a);
-        else if (D == 128 && bwd_adma()) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP, 2, true>), grid, 256, lds, st, a);
-        else if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }

@@ -180,6 +180,9 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
 
     // prologue: k-steps 0-3 in flight (clamped: a short block re-stages its last k-step), 0 and 1 landed, F_0 read,
     // then a barrier so slot 0 may be restaged during k-step 0
+    // the DMA descriptors / offsets may be fresh from v_readfirstlane (a VALU write of an SGPR that an inline-asm
+    // buffer_load reads needs 5 wait states the compiler cannot see)
+    asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int sa_ = soff_a(u), sb_ = soff_b(u);

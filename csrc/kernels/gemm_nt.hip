@@ -181,6 +181,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     }
 
     // prologue: stages 0 and 1 in flight, stage 0 landed, barrier, F0 of stage 0
+    // the DMA descriptors / offsets may be fresh from v_readfirstlane (a VALU write of an SGPR that an inline-asm
+    // buffer_load reads needs 5 wait states the compiler cannot see)
+    asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 16; ++p) NT_PIECE(p, 0, 0)
 #pragma unroll
@@ -270,6 +273,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         NT5_ROTATE()                                                                                              \
     }
     // prologue: stages 0 and 1 in flight (A[0] B[0], A[1] B[1]), stage 0 landed, barrier, F0 of stage 0
+    // the DMA descriptors / offsets may be fresh from v_readfirstlane (a VALU write of an SGPR that an inline-asm
+    // buffer_load reads needs 5 wait states the compiler cannot see)
+    asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         NT_PIECE_AT(false, i, lds0, 0)

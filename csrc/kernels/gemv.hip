@@ -223,25 +223,14 @@ __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int6
 }
 
 int rows_per_wave(bool norm, int N) {
-    static const int env = [] {
-        const char* e = std::getenv("SCALING_AMD_GEMV_RPW");
-        return e ? std::atoi(e) : 0;
-    }();
-    const int r = env > 0 ? env : (norm ? 2 : 1);
+    const int r = norm ? 2 : 1;  // two rows per wave amortise the folded norm's pass over x (profiles/decode_r3b.log)
     return (r == 2 && N % 2 == 0) ? 2 : 1;
 }
 
 // waves per output row (cold-cache micro-benchmark, tools/gemv_bench.py): 4 for the NORM and SwiGLU kernels (their
 // per-piece work on x / gamma / two weight rows wants more waves in flight) and for long rows over few outputs
-// (the 4096 x 11008 down projection), 1 for the plain projections; SCALING_AMD_GEMV_KSPLIT=0/1 forces it off/on
-int waves_per_row(bool split) {
-    static const int env = [] {
-        const char* e = std::getenv("SCALING_AMD_GEMV_KSPLIT");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (env >= 0) return env > 0 ? 4 : 1;
-    return split ? 4 : 1;
-}
+// (the 4096 x 11008 down projection), 1 for the plain projections
+int waves_per_row(bool split) { return split ? 4 : 1; }
 
 template <int EPI, typename E, bool NORM, int RPW, int KS>
 void launch_k(int M, const void* x, int64_t ldx, const void* W, int64_t ldw, const void* b, const void* r, int64_t ldr,

@@ -337,21 +337,12 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
     IO<T>::st(out, c, s);
 }
 
-// SCALING_AMD_NORM_ROW_KERNEL=0 keeps decode-sized rows on the many-row kernel (A/B switch; results are bit-identical)
-static bool row_kernel_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("SCALING_AMD_NORM_ROW_KERNEL");
-        return !(e != nullptr && e[0] == '0');
-    }();
-    return on;
-}
-
 template <typename T, bool LAYER>
 static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int64_t rows,
                          int H, float eps, const void* res, void* sum_out, hipStream_t st) {
     const int nv = (H + 511) / 512;
     dim3 grid(cdiv(rows, 4)), block(256);
-    if (rows <= 4 && H <= 4096 && row_kernel_enabled()) {  // decode-sized (NV <= 8)
+    if (rows <= 4 && H <= 4096) {  // decode-sized (NV <= 8): one wave per row (profiles/decode_norm_row_ab_r2.log)
 #define SA_NR(N)                                                                                                   \
     hipLaunchKernelGGL((norm_fwd_row_kernel<T, N, LAYER>), dim3((unsigned)rows), dim3(64), 0, st, (const T*)x,      \
                        (const T*)w, (const T*)b, (T*)y, mean, rstd, H, eps, (const T*)res, (T*)sum_out)
