@@ -121,3 +121,49 @@ def _row_chunked_case(sp: bool, chunks: int):
 @pytest.mark.parametrize("sp,chunks", [(False, 2), (False, 4), (True, 2), (True, 4)])
 def test_row_parallel_chunked_matches_unchunked(sp, chunks):
     assert all(run_distributed(_row_chunked_case, 2, sp=sp, chunks=chunks).values())
+
+
+def _chunked_save_matmuls_case(sp: bool):
+    """``tensor_parallel_comm_chunks`` > 1 under ``every_layer_save_matmuls``: the checkpoint recompute replays the
+    piecewise GEMM + collective output instead of running it again (one forward call, no second collective), and the
+    gradients equal plain per-layer checkpointing."""
+    import scaling_amd.core.nn.linear.tp_overlap as tpo
+    from scaling_amd.core.nn.linear import RowParallelLinear
+    from scaling_amd.core.nn.parallel_module.activation_checkpointing import checkpoint_with_rng
+
+    topo = make_topology(model_parallel_size=2, sequence_parallel=sp, tensor_parallel_comm_chunks=2)
+    rank = topo.model_parallel_rank
+    m = RowParallelLinear(32, 24, bias=False, topology=topo, parallel_input=True, parallel_output=sp)
+    torch.manual_seed(7 + rank)
+    with torch.no_grad():
+        m.weight.normal_()
+    real = tpo._chunked_forward
+    calls = []
+
+    def counting(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+
+    grads = {}
+    for keep in (False, True):
+        calls.clear()
+        m.weight.grad = None
+        torch.manual_seed(11 + rank)
+        x = torch.randn(4, 16, 16, requires_grad=True)
+        fn = (lambda t: m.forward_sequence_parallel(t)) if sp else (lambda t: m(t))
+        tpo._chunked_forward = counting
+        try:
+            y = checkpoint_with_rng(fn, topo, True, x, keep_gemms=keep)
+            (y * y).sum().backward()
+        finally:
+            tpo._chunked_forward = real
+        assert len(calls) == (1 if keep else 2), (keep, len(calls))
+        grads[keep] = (x.grad.clone(), m.weight.grad.clone())
+    for a, b in zip(grads[False], grads[True]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    return True
+
+
+@pytest.mark.parametrize("sp", [False, True])
+def test_row_parallel_chunked_under_save_matmuls(sp):
+    assert all(run_distributed(_chunked_save_matmuls_case, 2, sp=sp).values())
