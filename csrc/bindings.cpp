@@ -160,9 +160,13 @@ at::Tensor rope(const at::Tensor& x, const at::Tensor& cosb, const at::Tensor& s
 
 // graph decode: q = RoPE(q heads) (returned), K cache[pos] = RoPE(k heads), V cache[pos] = v heads, one launch;
 // qkv: the projection row [1, nq + 2 nkv, hd] (contiguous), caches [cap, nkv, hd] (contiguous), pos [1] int64
+static bool err_word(const at::Tensor& e) {
+    return e.is_cuda() && e.scalar_type() == at::kInt && e.numel() >= 1;
+}
 c10::optional<at::Tensor> rope_kv_append(const at::Tensor& qkv, const at::Tensor& cosb, const at::Tensor& sinb,
                                          const at::Tensor& pos, int64_t nq, int64_t nkv, int64_t rot_dim, bool interleaved,
-                                         at::Tensor kc, at::Tensor vc) {
+                                         at::Tensor kc, at::Tensor vc, at::Tensor err) {
+    TORCH_CHECK(err_word(err), "rope_kv_append: err must be an int32 GPU tensor");
     check_cuda(qkv, "qkv");
     const int64_t hd = qkv.size(-1);
     if (!(qkv.is_contiguous() && qkv.numel() == (nq + 2 * nkv) * hd && kc.is_contiguous() && vc.is_contiguous() &&
@@ -176,7 +180,8 @@ c10::optional<at::Tensor> rope_kv_append(const at::Tensor& qkv, const at::Tensor
     auto q = at::empty({1, nq, hd}, qkv.options());
     if (!sa_launch::rope_kv_append(dt(qkv), interleaved, qkv.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(),
                                    pos.data_ptr<int64_t>(), cosb.data_ptr<float>(), sinb.data_ptr<float>(), (int)nq,
-                                   (int)nkv, (int)hd, (int)rot_dim, cur_stream()))
+                                   (int)nkv, (int)hd, (int)rot_dim, std::min<int64_t>(kc.size(0), cosb.size(0)),
+                                   err.data_ptr<int>(), cur_stream()))
         return c10::nullopt;
     return q;
 }
@@ -417,7 +422,9 @@ std::vector<at::Tensor> gemv_norm(const at::Tensor& x, c10::optional<at::Tensor>
 // rotary dims rd of hd; x one token).  None when the operands do not fit (the caller runs gemv_norm + rope_kv_append).
 c10::optional<at::Tensor> gemv_norm_rope(const at::Tensor& x, const at::Tensor& gamma, double eps, const at::Tensor& W,
                                          const at::Tensor& cosb, const at::Tensor& sinb, const at::Tensor& pos,
-                                         int64_t nq, int64_t nkv, int64_t rd, at::Tensor kc, at::Tensor vc) {
+                                         int64_t nq, int64_t nkv, int64_t rd, at::Tensor kc, at::Tensor vc,
+                                         at::Tensor err) {
+    TORCH_CHECK(err_word(err), "gemv_norm_rope: err must be an int32 GPU tensor");
     if (!gemv_norm_ok(x, W, gamma) || x.size(0) != 1) return c10::nullopt;
     if (!(kc.is_cuda() && kc.dim() == 3 && kc.is_contiguous() && vc.is_contiguous() && vc.sizes() == kc.sizes() &&
           kc.size(1) == nkv && kc.scalar_type() == x.scalar_type() && vc.scalar_type() == x.scalar_type()))
@@ -431,7 +438,8 @@ c10::optional<at::Tensor> gemv_norm_rope(const at::Tensor& x, const at::Tensor& 
     const at::DeviceGuard g(x.device());
     auto q = at::empty({1, nq, hd}, x.options());
     GemvRope r{cosb.data_ptr<float>(), sinb.data_ptr<float>(), pos.data_ptr<int64_t>(), q.data_ptr(), kc.data_ptr(),
-               vc.data_ptr(), (int)nq, (int)nkv, (int)hd, (int)rd};
+               vc.data_ptr(), (int)nq, (int)nkv, (int)hd, (int)rd, std::min<int64_t>(kc.size(0), cosb.size(0)),
+               err.data_ptr<int>()};
     sa_launch::gemv(dt(x), 1, x.data_ptr(), x.stride(0), W.data_ptr(), W.stride(0), nullptr, nullptr, 0,
                     (int)W.size(0), (int)W.size(1), cur_stream(), 3, nullptr, 0, gamma.data_ptr(), nullptr, nullptr,
                     (float)eps, &r);

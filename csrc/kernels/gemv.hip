@@ -46,6 +46,8 @@ struct NormArgs {
     E* kc;
     E* vc;
     int nq, nkv, hd, rd;
+    int64_t lim;  // position bound: min(cache rows, rotary table rows)
+    int* err;     // set when the position is out of [0, lim): nothing is written to the caches
 };
 
 // Streams this wave's share of K -- pieces g0, g0 + GS, ... (GS = 64 x waves per row) -- of NR weight rows against
@@ -190,6 +192,14 @@ __global__ __launch_bounds__(256) void gemv_kernel(const E* __restrict__ x, int6
             const float v0 = rnd<E>(acc[0][0]), v1 = rnd<E>(acc[1][0]);  // the projection's bf16 outputs
             const int h = row / na.hd, d = row - h * na.hd;
             const int64_t ps = na.pos[0];
+            if (ps < 0 || ps >= na.lim) {  // out-of-range position: no cache write, q zeroed, error word set
+                if (row == 0) *na.err = 1;
+                if (h < na.nq) {
+                    IO<E>::st(na.q_out + (int64_t)h * na.hd, d, 0.f);
+                    IO<E>::st(na.q_out + (int64_t)h * na.hd, d + 1, 0.f);
+                }
+                return;
+            }
             float o0 = v0, o1 = v1;
             E* dst;
             if (h < na.nq + na.nkv) {
@@ -301,12 +311,12 @@ void gemv(int dtype, int M, const void* x, int64_t ldx, const void* W, int64_t l
     if (dtype == DT_F16) {
         const NormArgs<_Float16> na{(const _Float16*)norm_w, (const _Float16*)norm_add, (_Float16*)norm_sum, eps,
                                     rp.cosb, rp.sinb, rp.pos, (_Float16*)rp.q_out, (_Float16*)rp.kc, (_Float16*)rp.vc,
-                                    rp.nq, rp.nkv, rp.hd, rp.rd};
+                                    rp.nq, rp.nkv, rp.hd, rp.rd, rp.lim, rp.err};
         launch_epi<_Float16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
     } else {
         const NormArgs<u16> na{(const u16*)norm_w, (const u16*)norm_add, (u16*)norm_sum, eps,
                                rp.cosb, rp.sinb, rp.pos, (u16*)rp.q_out, (u16*)rp.kc, (u16*)rp.vc,
-                               rp.nq, rp.nkv, rp.hd, rp.rd};
+                               rp.nq, rp.nkv, rp.hd, rp.rd, rp.lim, rp.err};
         launch_epi<u16>(epi, M, x, ldx, W, ldw, b, res, ldr, y, ldy, N, K, st, na);
     }
 }

@@ -26,8 +26,10 @@ void rope(int dtype, bool interleaved, const void* x, int64_t x_tok, int64_t x_h
           int64_t o_head, const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd,
           int seq_len, float sign, hipStream_t st);
 // graph decode: RoPE(q) -> q_out, RoPE(k) -> K cache row *pos, v -> V cache row *pos (one token); false = unsupported
+// lim = min(cache rows, rotary table rows); a position outside [0, lim) writes nothing but zeros into q and sets *err
 bool rope_kv_append(int dtype, bool interleaved, const void* x, void* q_out, void* kc, void* vc, const int64_t* pos,
-                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, hipStream_t st);
+                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, int64_t lim, int* err,
+                    hipStream_t st);
 }  // namespace sa_launch
 
 namespace sa_launch {
@@ -157,6 +159,7 @@ struct GemvRope {
     const float* cosb; const float* sinb; const int64_t* pos;
     void* q_out; void* kc; void* vc;
     int nq, nkv, hd, rd;
+    int64_t lim; int* err;  // position bound (min(cache rows, rotary table rows)); out of range: no write, *err = 1
 };
 namespace sa_launch {
 // gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ b) for M <= 4 (decode-time linear layers), bf16 / fp16, K % 8 == 0

@@ -159,16 +159,27 @@ __global__ __launch_bounds__(256) void rope_kernel(const T* __restrict__ x, T* _
 // projection row [nq + 2 nkv heads][hd] (contiguous); q heads are rotated into q_out [nq][hd]; k heads are rotated
 // straight into row *pos of the K cache and v heads copied into row *pos of the V cache ([cap][nkv][hd] each) --
 // replacing rope(q), rope(k) and two index_copy launches.  One work item = 8 pair slots (as rope_v8_kernel).
+// lim = min(cache rows, rotary table rows): a position outside [0, lim) writes no cache row, zeros q and sets *err
+// (the caller checks the word on the host; an out-of-range row index would otherwise write past the cache silently).
 template <typename T, bool IL>
 __global__ __launch_bounds__(256) void rope_kv_append_kernel(const T* __restrict__ x, T* __restrict__ q_out,
                                                              T* __restrict__ kc, T* __restrict__ vc,
                                                              const int64_t* __restrict__ pos, const float* cosb,
-                                                             const float* sinb, int nq, int nkv, int hd, int rd) {
+                                                             const float* sinb, int nq, int nkv, int hd, int rd,
+                                                             int64_t lim, int* __restrict__ err) {
     const int half = rd / 2;
     const int rc = IL ? rd / 8 : half / 8;
     const int CR = rc + (hd - rd) / 8;
     const int nh = nq + 2 * nkv;
     const int64_t ps = pos[0];
+    if (ps < 0 || ps >= lim) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *err = 1;
+        for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nq * hd / 8; i += gridDim.x * blockDim.x) {
+            const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            V8<T>::st(q_out + 8 * i, z);
+        }
+        return;
+    }
     const int n = nh * CR;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int h = i / CR, c = i - h * CR;
@@ -229,13 +240,14 @@ static int grid_for(int64_t n) {
 
 namespace sa_launch {
 bool rope_kv_append(int dtype, bool interleaved, const void* x, void* q_out, void* kc, void* vc, const int64_t* pos,
-                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, hipStream_t st) {
+                    const float* cosb, const float* sinb, int nq, int nkv, int hd, int rd, int64_t lim, int* err,
+                    hipStream_t st) {
     if (dtype == DT_F32 || hd % 8 || (interleaved ? rd % 8 : rd % 16)) return false;
     const int CR = (interleaved ? rd / 8 : rd / 16) + (hd - rd) / 8;
     const int g = grid_for((int64_t)(nq + 2 * nkv) * CR);
 #define SA_RKV(TT, IL)                                                                                            \
     hipLaunchKernelGGL((rope_kv_append_kernel<TT, IL>), g, 256, 0, st, (const TT*)x, (TT*)q_out, (TT*)kc, (TT*)vc, \
-                       pos, cosb, sinb, nq, nkv, hd, rd)
+                       pos, cosb, sinb, nq, nkv, hd, rd, lim, err)
     if (dtype == DT_BF16) { if (interleaved) SA_RKV(u16, true); else SA_RKV(u16, false); }
     else { if (interleaved) SA_RKV(f16, true); else SA_RKV(f16, false); }
 #undef SA_RKV

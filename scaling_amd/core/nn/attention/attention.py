@@ -179,10 +179,19 @@ class DecodeState:
     def __init__(self, n_prompt: int, device: torch.device) -> None:
         self.pos = torch.full((1,), n_prompt, dtype=torch.long, device=device)
         self.cu_k = torch.tensor([0, n_prompt + 1], dtype=torch.int32, device=device)
+        # set by the fused decode kernels when ``pos`` is outside the cache / rotary table (nothing is written then)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
 
     def reset(self, n_prompt: int) -> None:
         self.pos.fill_(n_prompt)
         self.cu_k[1:].fill_(n_prompt + 1)
+        self.err.zero_()
+
+    def check(self) -> None:
+        """Raises if a decode step ran at a position outside its cache (one host read of the error word)."""
+        if int(self.err.item()) != 0:
+            raise RuntimeError("graph decode: a step's position exceeded the static KV cache or the rotary table; "
+                               "its K/V rows were not written")
 
     def advance(self) -> None:
         self.pos.add_(1)
@@ -442,7 +451,7 @@ class ParallelSelfAttention(torch.nn.Module):
             return None
         q = ext().gemv_norm_rope(x2, nw[0], nw[1], w, re.cos_table, re.sin_table, kv.state.pos,
                                  self.num_attention_heads_per_partition, self.num_kv_heads_per_partition, re.dimensions,
-                                 kv.k, kv.v)
+                                 kv.k, kv.v, kv.state.err)
         if q is None:
             return None
         return q, kv.k, kv.v, kv.state.cu_k
@@ -540,8 +549,8 @@ class ParallelSelfAttention(torch.nn.Module):
                 and k.data_ptr() == base.data_ptr() + nq * hd * es and v.data_ptr() == base.data_ptr() + (nq + nkv) * hd * es
                 and q.stride(1) == hd and k.stride(1) == hd and v.stride(1) == hd):
             return None
-        qr = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), re.cos_table, re.sin_table, kv.state.pos, nq, nkv, re.dimensions, re.interleaved,
-                                  kv.k, kv.v)
+        qr = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), re.cos_table, re.sin_table, kv.state.pos, nq, nkv,
+                                  re.dimensions, re.interleaved, kv.k, kv.v, kv.state.err)
         if qr is None:
             return None
         return qr, kv.k, kv.v, kv.state.cu_k

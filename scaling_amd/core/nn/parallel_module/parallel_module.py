@@ -17,6 +17,7 @@ from typing import Any, Callable, Generic, NamedTuple, Optional, Union
 import torch
 import torch.distributed as dist
 
+from ....parallel import custom_allreduce
 from ...data import BaseLayerIO
 from ...optimizer.allreduce import allreduce_tensor_in_float32
 from ...optimizer.base import BaseOptimizer
@@ -332,6 +333,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                     raise NotImplementedError(f"Instruction '{ins.__class__.__name__}' not implemented")
         loss, metrics = self.get_loss(metrics_aggregation_fn)
         self.wait_pending_sends()
+        custom_allreduce.raise_on_errors()  # forward-only: no optimizer step reads the one-shot error words
         self.profiler.flush()
         self.step_timer.stop()
         self._layers.train()
@@ -354,6 +356,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
             else:
                 raise NotImplementedError(f"Instruction '{ins.__class__.__name__}' not implemented for run_instructions.")
         self.wait_pending_sends()
+        custom_allreduce.raise_on_errors()
         topo = self.topology
         if batch is not None and topo.config.pipe_parallel_size == 1 and ins is not None:
             out = self.pipe_buffer.take(BufferType.PIPELINE_STAGE_OUTPUT, ins.buffer_id)

@@ -275,6 +275,7 @@ class Optimizer(BaseOptimizer):
         v = vals.tolist()
         if v[2] > 0:
             custom_allreduce.reset_error_words()
+            custom_allreduce.disable_all()  # the communicators' epoch state is out of step: RCCL from here on
             raise RuntimeError("one-shot tensor-parallel all-reduce timed out waiting for a peer on some rank; "
                                "its outputs were poisoned (NaN) and this step's gradients are invalid")
         return float(v[0]), float(v[1])

@@ -11,8 +11,10 @@ protocol is exercised by a 2-process test on one GPU; multi-GPU xGMI runs are no
 
 Safety: enabling is a GROUP decision (every rank allocates / maps, then a MIN all-reduce of the per-rank success
 flag; all ranks use the path or none does), and a flag-wait timeout in the kernel poisons the output with NaN and
-sets the communicator's error word, which ``pending_error_words`` hands to the optimizer's per-step host read
-(``Optimizer._grad_stats``) so the step raises instead of training on garbage.
+sets the communicator's error word.  Training reads the words once per step on the host (``Optimizer._grad_stats``,
+one all-reduce with the grad norm) and raises instead of training on garbage; forward-only use (inference,
+``generate``, evaluation steps) calls ``raise_on_errors`` once per call.  After a timeout every communicator is
+retired (``disable_all``): its epoch / slot state is out of step across the ranks, so later calls fall back to RCCL.
 """
 from __future__ import annotations
 
@@ -138,3 +140,24 @@ def reset_error_words() -> None:
     for ar in _REGISTRY.values():
         if ar is not None:
             ar.err.zero_()
+
+
+def disable_all() -> None:
+    """Retires every communicator after a peer timeout: the group falls back to RCCL from here on (the one-shot
+    protocol's epoch / double-buffered slot state is no longer in step across the ranks).  The peer mappings stay
+    open until process exit (a rank may still be inside a kernel reading them)."""
+    for group in list(_REGISTRY):
+        _REGISTRY[group] = None
+
+
+def raise_on_errors() -> None:
+    """Host check of the error words (one small device read): raises RuntimeError and retires the communicators if
+    a one-shot all-reduce timed out since the last check.  For forward-only paths; training checks per step."""
+    errs = pending_error_words()
+    if not errs:
+        return
+    if int(torch.stack(errs).sum().item()) > 0:
+        reset_error_words()
+        disable_all()
+        raise RuntimeError("one-shot tensor-parallel all-reduce timed out waiting for a peer; its outputs were "
+                           "poisoned (NaN); the one-shot path is disabled, RCCL is used from here on")

@@ -99,6 +99,7 @@ class GraphDecoder:
             for _ in range(n):
                 self.graph.replay()
             done += n
+            self.state.check()
             got = self.tokens[:done].tolist()
             hit = next((i for i, t in enumerate(got) if t in stops), None)
             if hit is not None:

@@ -61,3 +61,32 @@ def test_enablement_succeeds_when_all_ranks_succeed():
     res = run_distributed(_worker, 2, timeout=120, fail_open_on=-1)
     assert {r[0] for r in res.values()} == {"enabled"}
     assert all(not r[1] and not r[2] for r in res.values())
+
+
+def test_error_word_raises_and_retires_communicators():
+    """A set error word (a peer timeout) makes ``raise_on_errors`` (forward-only paths) raise, clears the word and
+    retires every communicator, so later calls use RCCL instead of the out-of-step one-shot protocol."""
+    import pytest
+
+    from scaling_amd.parallel import custom_allreduce as ca
+
+    class _Comm:
+        def __init__(self) -> None:
+            self.err = torch.zeros(1, dtype=torch.int32)
+
+    saved = dict(ca._REGISTRY)
+    try:
+        ca._REGISTRY.clear()
+        a, b = _Comm(), _Comm()
+        ca._REGISTRY.update({"g0": a, "g1": b})
+        ca.raise_on_errors()  # healthy: no-op
+        assert ca._REGISTRY["g0"] is a
+        b.err.fill_(1)
+        with pytest.raises(RuntimeError, match="timed out"):
+            ca.raise_on_errors()
+        assert int(b.err.item()) == 0
+        assert ca._REGISTRY == {"g0": None, "g1": None}
+        assert ca.pending_error_words() == []
+    finally:
+        ca._REGISTRY.clear()
+        ca._REGISTRY.update(saved)

@@ -885,8 +885,9 @@ def test_gemv_norm_rope_matches_unfused(rot_frac):
     vc = torch.randn(cap, nkv, hd, device=DEV, dtype=torch.bfloat16)
     kc_ref, vc_ref = kc.clone(), vc.clone()
     _, base = ext().gemv_norm(x, None, g, 1e-5, w, 0)
-    q_ref = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), cos, sin, pos, nq, nkv, rd, True, kc_ref, vc_ref)
-    q = ext().gemv_norm_rope(x, g, 1e-5, w, cos, sin, pos, nq, nkv, rd, kc, vc)
+    err = torch.zeros(1, device=DEV, dtype=torch.int32)
+    q_ref = ext().rope_kv_append(base.view(1, nq + 2 * nkv, hd), cos, sin, pos, nq, nkv, rd, True, kc_ref, vc_ref, err)
+    q = ext().gemv_norm_rope(x, g, 1e-5, w, cos, sin, pos, nq, nkv, rd, kc, vc, err)
     assert q is not None and q_ref is not None
     torch.testing.assert_close(q, q_ref, atol=1e-2, rtol=1e-2)
     torch.testing.assert_close(kc, kc_ref, atol=1e-2, rtol=1e-2)
@@ -894,8 +895,13 @@ def test_gemv_norm_rope_matches_unfused(rot_frac):
     other = torch.ones(cap, dtype=torch.bool, device=DEV)
     other[29] = False
     assert torch.equal(kc[other], kc_ref[other])  # only the position's row was written
+    assert int(err.item()) == 0
     assert ext().gemv_norm_rope(torch.randn(2, K, device=DEV, dtype=torch.bfloat16), g, 1e-5, w, cos, sin, pos, nq,
-                                nkv, rd, kc, vc) is None  # one token only
+                                nkv, rd, kc, vc, err) is None  # one token only
+    # a position past the cache: nothing written, q zeroed, the error word set (no silent out-of-bounds write)
+    kc0, vc0 = kc.clone(), vc.clone()
+    q = ext().gemv_norm_rope(x, g, 1e-5, w, cos, sin, torch.tensor([cap], device=DEV), nq, nkv, rd, kc, vc, err)
+    assert int(err.item()) == 1 and torch.equal(kc, kc0) and torch.equal(vc, vc0) and not q.any()
 
 
 def test_decode_layer_norm_gemv_matches_unfused():
@@ -940,9 +946,15 @@ def test_rope_kv_append_bit_identical(interleaved, rot_frac):
     k_ref = ext().rope(qkv[:, nq:nq + nkv], cos, sin, pos, rd, 1, interleaved, False)
     kc_ref.index_copy_(0, pos, k_ref)
     vc_ref.index_copy_(0, pos, qkv[:, nq + nkv:])
-    q = ext().rope_kv_append(qkv, cos, sin, pos, nq, nkv, rd, interleaved, kc, vc)
+    err = torch.zeros(1, device=DEV, dtype=torch.int32)
+    q = ext().rope_kv_append(qkv, cos, sin, pos, nq, nkv, rd, interleaved, kc, vc, err)
     assert q is not None
-    assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+    assert torch.equal(q, q_ref) and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref) and int(err.item()) == 0
+    # positions outside [0, cap): no cache row written, q zeroed, the error word set
+    for bad in (cap, cap + 5, -1):
+        err.zero_()
+        q = ext().rope_kv_append(qkv, cos, sin, torch.tensor([bad], device=DEV), nq, nkv, rd, interleaved, kc, vc, err)
+        assert int(err.item()) == 1 and not q.any() and torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
 
 
 @pytest.mark.parametrize("T,H,F", [(512, 256, 512), (1024, 512, 768)])
