@@ -580,8 +580,13 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
                                const at::Tensor& o, const at::Tensor& lse, const at::Tensor& cu_q, const at::Tensor& cu_k,
                                int64_t max_q, int64_t max_k, double scale, bool causal, int64_t window,
                                const c10::optional<at::Tensor>& dq_out, const c10::optional<at::Tensor>& dk_out,
-                               const c10::optional<at::Tensor>& dv_out, double p_drop, int64_t seed, int64_t local_heads) {
+                               const c10::optional<at::Tensor>& dv_out, double p_drop, int64_t seed, int64_t local_heads,
+                               const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
+                               const c10::optional<at::Tensor>& rope_pos, int64_t rope_dim, int64_t rope_seq,
+                               bool rope_interleaved) {
     // d*_out: write the gradients into caller-provided strided views (e.g. slices of one dQKV buffer)
+    // rope_*: dq / dk leave rotated back by the inverse RoPE (the forward rotated q / k): folded into the dQ / dK
+    // epilogues where the layout allows it, else the stand-alone rope kernel runs on dq / dk afterwards
     check_qkv(q, "q"); check_qkv(k, "k"); check_qkv(v, "v"); check_qkv(o, "o");
     TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() && o.scalar_type() == q.scalar_type() &&
                 dout.scalar_type() == q.scalar_type(), "fa_bwd: dtypes differ");
@@ -626,9 +631,34 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
         a.dk_part = part[0].data_ptr<float>();
         a.dv_part = part[1].data_ptr<float>();
     }
+    const bool rope = rope_cos.has_value();
+    bool fold = false;
+    if (rope) {
+        TORCH_CHECK(rope_sin.has_value() && rope_cos->scalar_type() == at::kFloat && rope_sin->scalar_type() == at::kFloat &&
+                    rope_cos->is_contiguous() && rope_sin->is_contiguous() && rope_cos->size(-1) == rope_dim / 2 &&
+                    (!rope_pos.has_value() || (rope_pos->scalar_type() == at::kLong && rope_pos->numel() == T)),
+                    "fa_bwd: rope tables / positions");
+        // NeoX pairs must sit in one lane (rot dims a multiple of 64), interleaved pairs in one 4-element group;
+        // with the dK head split the partials are summed in fa_bwd_reduce_kernel, which does not rotate
+        fold = D >= 64 && rope_dim <= D && (rope_interleaved ? rope_dim % 8 == 0 : rope_dim % 64 == 0) &&
+               a.hsplit == 1 && Tk == T;
+        if (fold) {
+            a.rcos = rope_cos->data_ptr<float>(); a.rsin = rope_sin->data_ptr<float>();
+            a.rpos = rope_pos.has_value() ? rope_pos->data_ptr<int64_t>() : nullptr;
+            a.rrd = (int)rope_dim; a.rseq = (int)rope_seq; a.ril = rope_interleaved ? 1 : 0;
+        }
+    }
     if (T > 0 && a.nseg > 0)
         sa_launch::fa_bwd(a, (const uint16_t*)o.data_ptr(), o.stride(0), o.stride(1), T, (int)D, (int)max_q, (int)max_k,
                           q.scalar_type() == at::kHalf, cur_stream());
+    if (rope && !fold) {
+        const int64_t* pp = rope_pos.has_value() ? rope_pos->data_ptr<int64_t>() : nullptr;
+        for (at::Tensor* t : {&dq, &dk})
+            sa_launch::rope(dt(*t), rope_interleaved, t->data_ptr(), t->stride(0), t->stride(1), t->data_ptr(),
+                            t->stride(0), t->stride(1), rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), pp,
+                            t->size(0), (int)t->size(1), (int)t->size(2), (int)rope_dim, (int)rope_seq, -1.f,
+                            cur_stream());
+    }
     return {dq, dk, dv};
 }
 // ------------------------------------------------------------------ masked softmax / activations / dropout
@@ -761,5 +791,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("spin_us", &spin_us, "debug: busy-wait kernel of ~us microseconds on the current stream");
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
     m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("max_k") = -1);
-    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1);
+    m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("rope_cos") = py::none(), py::arg("rope_sin") = py::none(), py::arg("rope_pos") = py::none(), py::arg("rope_dim") = 0, py::arg("rope_seq") = 1, py::arg("rope_interleaved") = false);
 }

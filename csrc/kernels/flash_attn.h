@@ -190,6 +190,11 @@ __device__ __forceinline__ u16 f2t(float f) {
     if constexpr (F16) return __builtin_bit_cast(u16, (_Float16)f);
     else return f2bf(f);
 }
+template <bool F16>
+__device__ __forceinline__ float t2f(u16 v) {
+    if constexpr (F16) return (float)__builtin_bit_cast(_Float16, v);
+    else return bf2f(v);
+}
 
 // ---- attention dropout: counter-based keep mask, a pure function of (seed, q head, query token, key
 // token), so the forward and both backward kernels (different lane <-> element layouts) regenerate the

@@ -81,6 +81,73 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// Stores one lane's gradient row (NT x 16 accumulators: element 4g + j of acc[t] is dim 32t + 8g + 4h + j) scaled by
+// `scale`, with the inverse RoPE of the row's token folded in when a.rcos is set -- the arithmetic of the stand-alone
+// rope kernel on the rounded gradient (round, rotate with rot_pair and sign -1, round), so the fold is bit-identical
+// to flash backward + rope(..., inverse).  NeoX pairs (d, d + rrd/2) sit in accumulators t and t + rrd/64 of the
+// same lane; interleaved pairs are elements (2p, 2p+1) of one 4-element group.
+template <int D, bool F16>
+__device__ __forceinline__ void store_grad_row(const BwdArgs& a, const f32x16 (&acc)[D / 32], float scale, int64_t tok,
+                                               int h, u16* dst) {
+    constexpr int NT = D / 32;
+    float v[NT][16];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[t][e] = t2f<F16>(f2t<F16>(acc[t][e] * scale));
+    if (a.rcos != nullptr) {
+        const int half = a.rrd / 2;
+        const int64_t ps = a.rpos ? a.rpos[tok] : (tok % a.rseq);
+        const float* cb = a.rcos + ps * half;
+        const float* sb = a.rsin + ps * half;
+        if (a.ril) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; j += 2) {
+                        const int d = 32 * t + 8 * g + 4 * h + j;
+                        if (d < a.rrd) {
+                            float o0, o1;
+                            rot_pair(v[t][4 * g + j], v[t][4 * g + j + 1], cb[d / 2], -sb[d / 2], o0, o1);
+                            v[t][4 * g + j] = o0;
+                            v[t][4 * g + j + 1] = o1;
+                        }
+                    }
+        } else {
+            const int pt = half / 32;  // partner accumulator offset
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int d = 32 * t + 8 * g + 4 * h + j;
+                        if (d < half) {
+#pragma unroll
+                            for (int t2 = 0; t2 < NT; ++t2)
+                                if (t2 == t + pt) {  // compile-time indexing of the partner (pt is uniform)
+                                    float o0, o1;
+                                    rot_pair(v[t][4 * g + j], v[t2][4 * g + j], cb[d], -sb[d], o0, o1);
+                                    v[t][4 * g + j] = o0;
+                                    v[t2][4 * g + j] = o1;
+                                }
+                        }
+                    }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            u16x4 w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(v[t][4 * g + j]);
+            *reinterpret_cast<u16x4*>(dst + 32 * t + 8 * g + 4 * h) = w;
+        }
+}
+
 // dK / dV: workgroup = 4 waves x 32 keys of one (segment, kv head); the key is on the MFMA lane.  Each
 // wave keeps its 32 K rows as register-resident B-operand fragments and reads its V rows from the
 // workgroup's V image (LDS, loaded once); it sweeps the GQA (sub)group's q heads x 32-query tiles.  Q, dO,
@@ -294,21 +361,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                     *reinterpret_cast<f32x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
                 }
         } else {
-            u16* kp = a.dk + (int64_t)(k0s + mykey) * a.dk_tok + (int64_t)hk * a.dk_head;
             u16* vp = a.dv + (int64_t)(k0s + mykey) * a.dv_tok + (int64_t)hk * a.dv_head;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    u16x4 wk, wv;
+                    u16x4 wv;
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        wk[j] = f2t<F16>(dk[t][4 * g + j] * a.scale);
-                        wv[j] = f2t<F16>(dv[t][4 * g + j]);
-                    }
-                    *reinterpret_cast<u16x4*>(kp + 32 * t + 8 * g + 4 * h) = wk;
+                    for (int j = 0; j < 4; ++j) wv[j] = f2t<F16>(dv[t][4 * g + j]);
                     *reinterpret_cast<u16x4*>(vp + 32 * t + 8 * g + 4 * h) = wv;
                 }
+            store_grad_row<D, F16>(a, dk, a.scale, k0s + mykey, h,
+                                   a.dk + (int64_t)(k0s + mykey) * a.dk_tok + (int64_t)hk * a.dk_head);
         }
     }
 #endif
@@ -446,18 +510,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_DQ_ISSUE
-    if (myq < Lq) {
-        u16* qp = a.dq + (int64_t)(q0s + myq) * a.dq_tok + (int64_t)hq * a.dq_head;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                u16x4 w;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(dq[t][4 * g + j] * a.scale);
-                *reinterpret_cast<u16x4*>(qp + 32 * t + 8 * g + 4 * h) = w;
-            }
-    }
+    if (myq < Lq)
+        store_grad_row<D, F16>(a, dq, a.scale, q0s + myq, h,
+                               a.dq + (int64_t)(q0s + myq) * a.dq_tok + (int64_t)hq * a.dq_head);
 #endif
 }
 

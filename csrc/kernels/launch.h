@@ -127,6 +127,10 @@ struct BwdArgs {
     int hsplit, Tk;
     float* dk_part;
     float* dv_part;
+    // inverse RoPE folded into the dQ / dK epilogues (rcos == nullptr: none): tables [max_pos][rrd / 2], positions
+    // rpos[token] or token % rseq, rotary dims rrd (NeoX pairs (i, i + rrd/2) need rrd % 64 == 0), interleaved pairs
+    const float* rcos; const float* rsin; const int64_t* rpos;
+    int rrd, rseq, ril;
 };
 namespace sa_launch {
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,

@@ -222,8 +222,9 @@ class _RopeFlashAttn(torch.autograd.Function):
     """RoPE on q/k + flash attention over views of ONE projection output (``base``).
 
     Backward allocates ``dbase`` once: the attention backward writes dq/dk/dv straight into its q/k/v
-    slices and the inverse rotation runs in place there, so no per-slice gradient buffers, zero-fills,
-    slice copies or gradient sums are materialised (autograd's view backward would do all of those)."""
+    slices with the inverse rotation applied in its dQ / dK epilogues (no RoPE pass over dq / dk), so no per-slice
+    gradient buffers, zero-fills, slice copies or gradient sums are materialised (autograd's view backward would do
+    all of those)."""
 
     @staticmethod
     def forward(ctx: Any, base, specs, cos, sin, pos, rot_dim, seq_len, interleaved, cu_q, cu_k, max_q, max_k, scale,
@@ -243,10 +244,9 @@ class _RopeFlashAttn(torch.autograd.Function):
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
         v = _view(base, specs[2])
+        # the inverse rotation of dq / dk is folded into the attention backward's dQ / dK epilogues
         ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
-                     local_heads)
-        ext().rope(dq, cos, sin, pos, rot_dim, seq_len, interleaved, True, dq)
-        ext().rope(dk, cos, sin, pos, rot_dim, seq_len, interleaved, True, dk)
+                     local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
         return (dbase,) + (None,) * 17
 
 

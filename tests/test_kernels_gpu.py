@@ -231,6 +231,29 @@ def test_rope_flash_attention_fused(qkv_in_one):
     torch.testing.assert_close(gf.float(), base.grad.float(), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("hd,rd,il,nq,nkv,S", [(128, 128, False, 8, 8, 256), (128, 64, False, 8, 8, 256),
+                                               (128, 128, True, 8, 8, 256), (64, 64, False, 4, 4, 192),
+                                               (128, 32, False, 8, 8, 256), (128, 128, False, 16, 2, 128)])
+def test_flash_bwd_rope_fold_bit_exact(hd, rd, il, nq, nkv, S):
+    """Inverse RoPE folded into the dQ / dK epilogues == flash backward then the stand-alone inverse rope, bit for
+    bit (NeoX full / partial, interleaved, head_dim 64; rot_dim 32 and the GQA head-split backward take the
+    unfolded path inside the binding)."""
+    torch.manual_seed(11)
+    T = 2 * S
+    q, k, v, do = (torch.randn(T, h, hd, device=DEV, dtype=torch.bfloat16) for h in (nq, nkv, nkv, nq))
+    cu = torch.arange(0, T + 1, S, device=DEV, dtype=torch.int32)
+    cos, sin = rope.rope_tables(rd, S, 10000, il, torch.bfloat16, DEV)
+    pos = torch.arange(S, device=DEV).repeat(2)
+    o, lse = ext().fa_fwd(q, k, v, cu, cu, S, hd ** -0.5, True, -1)
+    args = (do, q, k, v, o, lse, cu, cu, S, S, hd ** -0.5, True, -1)
+    dq, dk, dv = ext().fa_bwd(*args)
+    ext().rope(dq, cos, sin, pos, rd, S, il, True, dq)
+    ext().rope(dk, cos, sin, pos, rd, S, il, True, dk)
+    for p in (pos, None):
+        fq, fk, fv = ext().fa_bwd(*args, None, None, None, 0.0, 0, -1, cos, sin, p, rd, S, il)
+        assert torch.equal(fq, dq) and torch.equal(fk, dk) and torch.equal(fv, dv)
+
+
 @pytest.mark.parametrize("V,offset", [(1000, 0), (32000, 0), (50257, 0), (1001, 0), (32000, 3)])
 def test_cross_entropy(V, offset):
     """Odd vocab sizes (rows not 16-B aligned) and a misaligned base take the scalar row path."""
