@@ -63,8 +63,9 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
                    choices=["disabled", "every_layer", "every_layer_keep_attention", "every_layer_save_matmuls",
                             "every_pipe_stage"])
     p.add_argument("--sequence-parallel", action="store_true")
-    p.add_argument("--tp-comm-chunks", type=int, default=1,
-                   help="row-parallel GEMM + TP all-reduce / SP reduce-scatter in this many overlapped token pieces")
+    p.add_argument("--tp-comm-chunks", type=int, default=0,
+                   help="row-parallel GEMM + TP all-reduce / SP reduce-scatter in this many overlapped token pieces; "
+                   "0 = chosen by comm_estimate.default_tp_comm_chunks (1 without TP)")
     p.add_argument("--zero", type=int, default=1)
     p.add_argument("--overlap-step", type=int, default=1,
                    help="run the optimizer update on a side stream, overlapped with the next forward (1) or inline (0)")
@@ -94,11 +95,11 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
 PRESETS: dict[str, dict[str, Any]] = {
     # "Llama-2-7B-shape TP=2 PP=1 DP=4 bf16 + ZeRO-1": Megatron-SP inside the TP pair (reduce-scatter / all-gather
     # instead of all-reduce, activations sharded), row-parallel GEMMs overlapped with their collective in 4 pieces
-    "baseline3": {"tp": 2, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": True, "tp_comm_chunks": 4,
+    "baseline3": {"tp": 2, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": True, "tp_comm_chunks": 0,
                   "activation_checkpointing": "disabled", "lora": False, "zero": 1},
     # "TP=2 PP=2 DP=2 (full 3D parallel, 1F1B pipeline) with activation checkpointing": 4 micro-batches of 4 keep the
     # two-stage pipe 4/5 busy; per-layer checkpointing as the reference's every_layer
-    "baseline4": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True, "tp_comm_chunks": 4,
+    "baseline4": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True, "tp_comm_chunks": 0,
                   "activation_checkpointing": "every_layer", "lora": False, "zero": 1},
     # "7B + LoRA fine-tune path, TP=1 PP=1 DP=8 ZeRO-1 (PEFT adapters exercised)"
     "baseline5": {"tp": 1, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": False, "tp_comm_chunks": 1,
@@ -217,6 +218,11 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
         arch["lora_config"] = {"name": "lora", "rank": a.lora_rank, "alpha": 16,
                                "parallel_modules": ["query", "key", "value", "dense"]}
         training.update(finetune=True, finetunable_parameters=["lora"])
+    if a.tp_comm_chunks == 0:  # auto: from the first-order xGMI / GEMM time model
+        from scaling_amd.transformer.utils.comm_estimate import default_tp_comm_chunks
+
+        a.tp_comm_chunks = default_tp_comm_chunks(hidden_size=arch["hidden_size"], tokens=a.micro_batch * a.seq_len,
+                                                  tp=a.tp)
     topo: dict[str, Any] = {
         "world_size": world, "global_rank": rank, "local_slot": local,
         "model_parallel_size": a.tp, "pipe_parallel_size": a.pp, "data_parallel_size": dp,

@@ -58,3 +58,28 @@ def comm_volume_estimate(*, hidden_size: int, num_layers: int, seq_len: int, mic
         "tp_ms": round(t_ms(tp_bytes, tp), 2), "pp_ms": round(t_ms(pp_bytes, 2), 2), "dp_ms": round(t_ms(dp_bytes, dp), 2),
         "assumptions": f"xGMI {XGMI_LINK_BYTES_PER_S / 1e9:.0f} GB/s/link x {link_efficiency}, no overlap",
     }
+
+
+def default_tp_comm_chunks(*, hidden_size: int, tokens: int, tp: int, in_features: int | None = None,
+                           precision: str = "bfloat16", gemm_flops_per_s: float = 1.2e15, chunk_latency_s: float = 25e-6,
+                           min_chunk_rows: int = 2048, link_efficiency: float = 0.7) -> int:
+    """Token pieces for the row-parallel GEMM + TP collective overlap (``tensor_parallel_comm_chunks``) from the
+    same first-order model: the collective of ``[tokens, hidden]`` takes ``tc`` on the TP group's links, the local
+    GEMM (``in_features / tp`` inputs, default the hidden size) takes ``tg`` at ``gemm_flops_per_s``; with ``n``
+    pieces ``min(tc, tg) (n-1)/n`` is hidden and every extra piece costs ``chunk_latency_s`` (collective launch +
+    a smaller, less efficient GEMM).  Pieces stay >= ``min_chunk_rows`` tokens.  Returns the best of 1, 2, 4, 8."""
+    if tp <= 1:
+        return 1
+    act = _dtype_bytes(precision)
+    k = (in_features or hidden_size) // tp
+    links = min(tp - 1, XGMI_LINKS_PER_GPU)
+    tc = 2.0 * (tp - 1) / tp * tokens * hidden_size * act / (XGMI_LINK_BYTES_PER_S * link_efficiency * links)
+    tg = 2.0 * tokens * k * hidden_size / gemm_flops_per_s
+    best, best_gain = 1, 0.0
+    for n in (2, 4, 8):
+        if tokens % n or tokens // n < min_chunk_rows:
+            break
+        gain = min(tc, tg) * (n - 1) / n - (n - 1) * chunk_latency_s
+        if gain > best_gain:
+            best, best_gain = n, gain
+    return best

@@ -112,3 +112,21 @@ def test_bench_preset_runs_gloo():
     res = _json_lines(r.stdout)[0]
     assert res["config"]["preset"] == "baseline4"
     assert res["config"]["parallelism"].startswith("tp2_pp2_dp1_zero1_ac-every_layer_sp")
+
+
+def test_default_tp_comm_chunks():
+    """Auto ``--tp-comm-chunks``: 1 without TP or for short micro-batches (pieces would fall under 2048 tokens),
+    more pieces when the TP collective is long enough to hide behind the GEMM."""
+    from scaling_amd.transformer.utils.comm_estimate import default_tp_comm_chunks as f
+
+    assert f(hidden_size=4096, tokens=8 * 4096, tp=1) == 1
+    assert f(hidden_size=4096, tokens=2048, tp=2) == 1
+    assert f(hidden_size=4096, tokens=8 * 2048, tp=2) == 4
+    assert f(hidden_size=4096, tokens=4 * 2048, tp=2) == 2
+    sys.path.insert(0, ROOT)
+    import bench
+
+    a = bench._args(["--gpus", "2", "--preset", "baseline3"])
+    assert a.tp_comm_chunks == 0  # resolved when the config is built
+    cfg = bench._config_dict(a, 2, 0, 0)
+    assert cfg["topology"]["tensor_parallel_comm_chunks"] == a.tp_comm_chunks >= 2
