@@ -751,7 +751,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
     m.def("gemm_nt_ok", &gemm_nt_ok, "whether gemm_nt supports these operands");
     m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16, 64-deep staged HIP kernel)");
-    m.def("gemm_nt_set_split5", &sa_launch::gemm_nt_set_split5, "A/B hook: five-image LDS pipeline (1) or two stages (0)");
     m.def("gemm_nt_swiglu_ok", &gemm_nt_swiglu_ok, "whether gemm_nt_swiglu supports these operands");
     m.def("gemm_nt_swiglu", &gemm_nt_swiglu, "h = silu(g) u, z = [g | u] from x @ [W_gate; W_up]^T (one kernel)");
     m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, "dz = swiglu_bwd(dY @ Wt^T, z) (one kernel)");

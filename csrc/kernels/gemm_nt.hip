@@ -12,16 +12,16 @@
 // stand-alone SwiGLU kernels (swiglu_rope.hip), so the fused and unfused paths agree.
 //
 // Structure (one 256x256 tile per workgroup, 4 waves = one per SIMD, each 128x128 of 16x16x32 MFMAs in AGPRs):
-//  * 64-deep k-stages, two LDS stage buffers of [256 rows][64 k] bf16 per operand (2 x 64 KiB);
+//  * 64-deep k-stages in five 32-KiB LDS images of [256 rows][64 k] bf16: A in two, B in three (see below);
 //  * LDS-DMA pieces (buffer_load ... lds) of 8 rows x 128 B: every lane group of 8 reads ONE full 128-B line
 //    (the previous 16-rows x 64-B pieces read half lines: twice the cache-line requests per byte);
 //  * image swizzle: 16-B chunk c of row r at c ^ ((r >> 1) & 7) -- every ds_read_b128 lane group of a fragment
 //    read hits 16 distinct 16-B bank slots (conflict-free), and the DMA source is permuted to match;
-//  * per stage t: sub-step 0 multiplies k 0-31 (registers F0) while reading k 32-63 (F1); wait for own reads and
-//    DMA, ONE barrier; sub-step 1 multiplies F1 while reading F0 of stage t+1 and issuing the DMA of stage t+2 into
-//    the buffer this stage just vacated.  The barrier both publishes stage t+1 and releases buffer t for restaging,
-//    so one barrier per 128 MFMAs (the 32-deep ring needed one per 64), and each DMA piece has two sub-steps
-//    (~128 MFMAs) to land.
+//  * per stage t: sub-step 0 multiplies k 0-31 (registers F0) while reading k 32-63 (F1) and issuing stage t+2's B
+//    pieces; wait for own reads and stage t+1, ONE barrier; sub-step 1 multiplies F1 while reading F0 of stage t+1
+//    and issuing stage t+2's A pieces.  One barrier per 128 MFMAs, 8 DMA pieces per sub-step (a schedule with two
+//    stage buffers had to issue all 16 in one sub-step: 1.25-1.30 PF against 1.37-1.46 for this one,
+//    profiles/gemm_nt_split5_ab_r4.log).
 //  * grid: XCD-aware bijective remap, then 8-row groups of tiles (the 32 tiles resident on one XCD share A/B panels
 //    in its L2).
 // Reference op: F.linear at src/scaling/core/nn/linear/column_parallel_linear.py:151 / row_parallel_linear.py:158,
@@ -38,8 +38,7 @@ using fa::bf16x8;
 using fa::lds_void;
 
 constexpr int kImg = 256 * 64 * 2;  // one operand's stage image [256][64] bf16
-constexpr int kStage = 2 * kImg;   // A + B
-constexpr int kLds = 2 * kStage;   // two stages
+constexpr int kLds = 5 * kImg;      // A[0..1] + B[0..2]: all 160 KiB of LDS
 
 __device__ __forceinline__ void mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
@@ -55,7 +54,7 @@ __device__ __forceinline__ void hard_barrier() {
 }
 __device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
 
-template <int EPI, bool SPLIT5>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
                                                          const u16* __restrict__ B, int ldb, uint32_t b_bytes, int M,
                                                          int N, int K, NtEpi ep) {
@@ -116,7 +115,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                          "v"(va), "s"(rsa), "s"(abase + (I) * astep + ku_)                                         \
                          : "m0");                                                                                 \
     }
-#define NT_PIECE(P, BUF, U) NT_PIECE_AT((P) & 1, (P) >> 1, lds0 + (BUF) * kStage + (((P) & 1) ? kImg : 0), U)
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -130,85 +128,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     // lane l holds row 16i + (l & 15) of its wave's 128 rows, k chunk 4h + (l >> 4) of the stage; stored chunk
     // = c ^ f(r), f = ((l & 15) >> 1)
     const int lo0 = fr * 128 + 16 * (fg ^ ff), lo1 = fr * 128 + 16 * ((fg ^ ff) ^ 4);
-    if constexpr (!SPLIT5) {
-    // ---- two stage buffers [A | B] of 64 KiB.  One opaque VGPR per (buffer, half, operand); fragment i in the
-    // ds_read immediate (i * 2048 + the B image's 32 KiB < 64 KiB).
-    // ---- fragments: lane l holds row 16i + (l & 15) of its wave's 128 rows, k chunk 4h + (l >> 4) of the stage;
-    // stored chunk = c ^ f(r), f = ((l & 15) >> 1).  One opaque VGPR per (buffer, half, operand); fragment i in the
-    // ds_read immediate (i * 2048 + the B image's 32 KiB < 64 KiB).
-    int oa[2][2], ob[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            oa[s][h] = s * kStage + wm * 128 * 128 + (h ? lo1 : lo0);
-            ob[s][h] = s * kStage + kImg + wn * 128 * 128 + (h ? lo1 : lo0);
-            asm volatile("" : "+v"(oa[s][h]), "+v"(ob[s][h]));
-        }
-
-    // sub-step 0 of stage U (buffer BUF): MFMAs on F0, F1 of the same stage read one fragment per 3 MFMAs over the
-    // first 48 (retired well before the waits); then own
-    // reads retired, own DMA landed (stage U+1), barrier
-#define NT_SUB0(BUF)                                                                                             \
-    {                                                                                                            \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {            \
-            mfma(acc[i][j], fb0[j], fa0[i]);                                                                     \
-            const int m_ = i * 8 + j;                                                                            \
-            if (m_ % 3 == 1 && m_ < 48) {                                                                        \
-                const int f_ = m_ / 3;                                                                           \
-                if (f_ < 8) fb1[f_] = frag(ob[BUF][1], f_);                                                      \
-                else fa1[f_ - 8] = frag(oa[BUF][1], f_ - 8);                                                     \
-            }                                                                                                    \
-        }                                                                                                        \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
-        wait_vm<0>();                                                                                            \
-        hard_barrier();                                                                                          \
-    }
-    // sub-step 1 of stage U: MFMAs on F1; F0 of stage U+1 from the other buffer (NEXT), DMA of stage U+2 into BUF
-    // (PIECES) one piece per 4 MFMAs
-#define NT_SUB1(BUF, U, NEXT, PIECES)                                                                            \
-    {                                                                                                            \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {            \
-            mfma(acc[i][j], fb1[j], fa1[i]);                                                                     \
-            const int m_ = i * 8 + j;                                                                            \
-            if ((NEXT) && m_ % 3 == 1 && m_ < 48) {                                                              \
-                const int f_ = m_ / 3;                                                                           \
-                if (f_ < 8) fb0[f_] = frag(ob[(BUF) ^ 1][0], f_);                                                \
-                else fa0[f_ - 8] = frag(oa[(BUF) ^ 1][0], f_ - 8);                                               \
-            }                                                                                                    \
-            if ((PIECES) && (m_ & 3) == 3) NT_PIECE(m_ >> 2, BUF, (U) + 2)                                      \
-        }                                                                                                        \
-    }
-
-    // prologue: stages 0 and 1 in flight, stage 0 landed, barrier, F0 of stage 0
-    // the DMA descriptors / offsets may be fresh from v_readfirstlane (a VALU write of an SGPR that an inline-asm
-    // buffer_load reads needs 5 wait states the compiler cannot see)
-    asm volatile("s_nop 4" ::: "memory");
-#pragma unroll
-    for (int p = 0; p < 16; ++p) NT_PIECE(p, 0, 0)
-#pragma unroll
-    for (int p = 0; p < 16; ++p) NT_PIECE(p, 1, 1)
-    wait_vm<16>();
-    hard_barrier();
-#pragma unroll
-    for (int f = 0; f < 16; ++f) {
-        if (f < 8) fb0[f] = frag(ob[0][0], f);
-        else fa0[f - 8] = frag(oa[0][0], f - 8);
-    }
-    int u = 0;
-    for (; u < T - 2; u += 2) {  // T even (K % 128 == 0, checked by the dispatcher)
-        NT_SUB0(0)
-        NT_SUB1(0, u, true, true)
-        NT_SUB0(1)
-        NT_SUB1(1, u + 1, true, true)
-    }
-    NT_SUB0(0)
-    NT_SUB1(0, u, true, false)
-    NT_SUB0(1)
-    NT_SUB1(1, u + 1, false, false)
-#undef NT_SUB0
-#undef NT_SUB1
-    } else {
     // ---- five 32-KiB images: A[0..1] at 0 / 32 KiB, B[0..2] at 64 / 96 / 128 KiB (all 160 KiB of LDS).  Stage s
     // lives in A[s % 2] and B[s % 3]; B's third buffer lets stage t+2's B image be staged during sub-step (t, 0)
     // (B[(t+2) % 3] was last read before barrier t-1) and its A image during (t, 1) (A[t % 2] was last read before
@@ -307,8 +226,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
 #undef NT5_SUB0
 #undef NT5_SUB1
 #undef NT5_ROTATE
-    }
-#undef NT_PIECE
 #undef NT_PIECE_AT
     wait_vm<0>();
     // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
@@ -387,18 +304,15 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         }
     }
 }
-#define SA_NT_INST(E, S5)                                                                                      \
-    template __global__ void gemm_nt_kernel<E, S5>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, \
-                                                   int, uint32_t, int, int, int, NtEpi);
-SA_NT_INST(EPI_STORE, false) SA_NT_INST(EPI_SWIGLU, false) SA_NT_INST(EPI_SWIGLU_BWD, false)
-SA_NT_INST(EPI_STORE, true) SA_NT_INST(EPI_SWIGLU, true) SA_NT_INST(EPI_SWIGLU_BWD, true)
+#define SA_NT_INST(E)                                                                                          \
+    template __global__ void gemm_nt_kernel<E>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int, \
+                                               uint32_t, int, int, int, NtEpi);
+SA_NT_INST(EPI_STORE) SA_NT_INST(EPI_SWIGLU) SA_NT_INST(EPI_SWIGLU_BWD)
 #undef SA_NT_INST
 
 }  // namespace sa_gemm_nt
 
 namespace sa_launch {
-static bool g_nt_split5 = true;
-void gemm_nt_set_split5(bool on) { g_nt_split5 = on; }
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
     return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
            lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
@@ -410,12 +324,8 @@ void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, in
     const int nwg = (int)((M / 256) * (N / 256));
     const uint32_t ab = (uint32_t)(M * lda * 2), bb = (uint32_t)(N * ldb * 2);
 #define SA_NT_LAUNCH(E)                                                                                         \
-    if (g_nt_split5)                                                                                            \
-        hipLaunchKernelGGL((gemm_nt_kernel<E, true>), dim3(nwg), dim3(256), 5 * kImg, st, (const u16*)A,       \
-                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep);              \
-    else                                                                                                        \
-        hipLaunchKernelGGL((gemm_nt_kernel<E, false>), dim3(nwg), dim3(256), kLds, st, (const u16*)A,          \
-                           (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
+    hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab,         \
+                       (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
     if (epi == EPI_SWIGLU) SA_NT_LAUNCH(EPI_SWIGLU);
     else if (epi == EPI_SWIGLU_BWD) SA_NT_LAUNCH(EPI_SWIGLU_BWD);
     else SA_NT_LAUNCH(EPI_STORE);

@@ -70,7 +70,6 @@ struct NtEpi {
 };
 namespace sa_launch {
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
-void gemm_nt_set_split5(bool on);
 void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                const NtEpi& ep, hipStream_t st);
 }  // namespace sa_launch

@@ -59,22 +59,9 @@ def main() -> None:
         ref = x[:2048].float() @ w.float().t()
         arms = {"hipblaslt": lambda: torch.nn.functional.linear(x, w)}
         if ext().gemm_nt_ok(x, w):
-            ext().gemm_nt_set_split5(False)
             ext().gemm_nt(x, w, c)
             r["err"] = ((c[:2048].float() - ref).abs().max() / ref.abs().max()).item()
-            ext().gemm_nt_set_split5(True)
-            ext().gemm_nt(x, w, c)
-            r["err5"] = ((c[:2048].float() - ref).abs().max() / ref.abs().max()).item()
-
-            def ours2():
-                ext().gemm_nt_set_split5(False)
-                ext().gemm_nt(x, w, c)
-
-            def ours5():
-                ext().gemm_nt_set_split5(True)
-                ext().gemm_nt(x, w, c)
-            arms["ours2"] = ours2
-            arms["ours5"] = ours5
+            arms["ours"] = lambda: ext().gemm_nt(x, w, c)
         ts = {k: [] for k in arms}
         for _ in range(a.rounds):
             for k, fn in arms.items():

@@ -21,19 +21,16 @@ def err(M, N, K, x=None, w=None):
     return (d.max() / ref.abs().max()).item(), bad.mean().item(), bad
 
 
-for s5 in (False, True):
-    ext().gemm_nt_set_split5(s5)
-    print("split5", s5, flush=True)
-    for (M, N, K) in [(256, 256, 128), (256, 256, 256), (256, 256, 1024), (256, 256, 4096), (512, 512, 4096),
-                      (2048, 2048, 4096), (4096, 4096, 4096)]:
-        e, frac, bad = err(M, N, K)
-        msg = f"M{M} N{N} K{K}: max_rel_err {e:.4f} bad_frac {frac:.4f}"
-        if frac > 0:
-            rows = bad.sum(1).nonzero().flatten()
-            cols = bad.sum(0).nonzero().flatten()
-            msg += (f" bad rows%256 {sorted(set((rows % 256).tolist()))[:16]}"
-                    f" bad cols%256 {sorted(set((cols % 256).tolist()))[:16]}")
-        print(msg, flush=True)
+for (M, N, K) in [(256, 256, 128), (256, 256, 256), (256, 256, 1024), (256, 256, 4096), (512, 512, 4096),
+                  (2048, 2048, 4096), (4096, 4096, 4096)]:
+    e, frac, bad = err(M, N, K)
+    msg = f"M{M} N{N} K{K}: max_rel_err {e:.4f} bad_frac {frac:.4f}"
+    if frac > 0:
+        rows = bad.sum(1).nonzero().flatten()
+        cols = bad.sum(0).nonzero().flatten()
+        msg += (f" bad rows%256 {sorted(set((rows % 256).tolist()))[:16]}"
+                f" bad cols%256 {sorted(set((cols % 256).tolist()))[:16]}")
+    print(msg, flush=True)
 M, N, K = 256, 256, 1024
 x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
 w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
