@@ -638,10 +638,10 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
                     rope_cos->is_contiguous() && rope_sin->is_contiguous() && rope_cos->size(-1) == rope_dim / 2 &&
                     (!rope_pos.has_value() || (rope_pos->scalar_type() == at::kLong && rope_pos->numel() == T)),
                     "fa_bwd: rope tables / positions");
-        // NeoX pairs must sit in one lane (rot dims a multiple of 64), interleaved pairs in one 4-element group;
-        // with the dK head split the partials are summed in fa_bwd_reduce_kernel, which does not rotate
-        fold = D >= 64 && rope_dim <= D && (rope_interleaved ? rope_dim % 8 == 0 : rope_dim % 64 == 0) &&
-               a.hsplit == 1 && Tk == T;
+        // NeoX pairs sit in one lane for a full rotation (partner accumulator t + D/64), interleaved pairs in one
+        // 4-element group; with the dK head split the partials are summed in fa_bwd_reduce_kernel, which does not rotate
+        fold = D >= 64 && (rope_interleaved ? rope_dim <= D && rope_dim % 8 == 0 : rope_dim == D) && a.hsplit == 1 &&
+               Tk == T;
         if (fold) {
             a.rcos = rope_cos->data_ptr<float>(); a.rsin = rope_sin->data_ptr<float>();
             a.rpos = rope_pos.has_value() ? rope_pos->data_ptr<int64_t>() : nullptr;

@@ -84,67 +84,64 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
 // Stores one lane's gradient row (NT x 16 accumulators: element 4g + j of acc[t] is dim 32t + 8g + 4h + j) scaled by
 // `scale`, with the inverse RoPE of the row's token folded in when a.rcos is set -- the arithmetic of the stand-alone
 // rope kernel on the rounded gradient (round, rotate with rot_pair and sign -1, round), so the fold is bit-identical
-// to flash backward + rope(..., inverse).  NeoX pairs (d, d + rrd/2) sit in accumulators t and t + rrd/64 of the
-// same lane; interleaved pairs are elements (2p, 2p+1) of one 4-element group.
+// to flash backward + rope(..., inverse).  NeoX (full rotation, rrd == D: the binding checks) pairs dims d, d + D/2 =
+// accumulators t and t + NT/2 of the same lane; interleaved pairs are elements (2p, 2p+1) of one 4-element group.
+// One 4-element group (two for a NeoX pair) is live at a time: the epilogue must not raise the kernel's register peak.
 template <int D, bool F16>
 __device__ __forceinline__ void store_grad_row(const BwdArgs& a, const f32x16 (&acc)[D / 32], float scale, int64_t tok,
                                                int h, u16* dst) {
     constexpr int NT = D / 32;
-    float v[NT][16];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) v[t][e] = t2f<F16>(f2t<F16>(acc[t][e] * scale));
-    if (a.rcos != nullptr) {
-        const int half = a.rrd / 2;
+    const bool rope = a.rcos != nullptr;
+    const float* cb = nullptr;
+    const float* sb = nullptr;
+    if (rope) {
         const int64_t ps = a.rpos ? a.rpos[tok] : (tok % a.rseq);
-        const float* cb = a.rcos + ps * half;
-        const float* sb = a.rsin + ps * half;
-        if (a.ril) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int j = 0; j < 4; j += 2) {
-                        const int d = 32 * t + 8 * g + 4 * h + j;
-                        if (d < a.rrd) {
-                            float o0, o1;
-                            rot_pair(v[t][4 * g + j], v[t][4 * g + j + 1], cb[d / 2], -sb[d / 2], o0, o1);
-                            v[t][4 * g + j] = o0;
-                            v[t][4 * g + j + 1] = o1;
-                        }
-                    }
-        } else {
-            const int pt = half / 32;  // partner accumulator offset
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int d = 32 * t + 8 * g + 4 * h + j;
-                        if (d < half) {
-#pragma unroll
-                            for (int t2 = 0; t2 < NT; ++t2)
-                                if (t2 == t + pt) {  // compile-time indexing of the partner (pt is uniform)
-                                    float o0, o1;
-                                    rot_pair(v[t][4 * g + j], v[t2][4 * g + j], cb[d], -sb[d], o0, o1);
-                                    v[t][4 * g + j] = o0;
-                                    v[t2][4 * g + j] = o1;
-                                }
-                        }
-                    }
-        }
+        cb = a.rcos + ps * (a.rrd / 2);
+        sb = a.rsin + ps * (a.rrd / 2);
     }
+    auto rd = [&](int t, int g, float (&x)[4]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = t2f<F16>(f2t<F16>(acc[t][4 * g + j] * scale));
+    };
+    auto st = [&](int t, int g, const float (&x)[4]) {
+        u16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(x[j]);
+        *reinterpret_cast<u16x4*>(dst + 32 * t + 8 * g + 4 * h) = w;
+    };
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            u16x4 w;
+            const int d0 = 32 * t + 8 * g + 4 * h;
+            float x[4];
+            if (rope && !a.ril) {  // NeoX, rrd == D
+                if (t >= NT / 2) continue;  // stored with its partner
+                float y[4];
+                rd(t, g, x);
+                rd(t + NT / 2, g, y);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(v[t][4 * g + j]);
-            *reinterpret_cast<u16x4*>(dst + 32 * t + 8 * g + 4 * h) = w;
+                for (int j = 0; j < 4; ++j) {
+                    float o0, o1;
+                    rot_pair(x[j], y[j], cb[d0 + j], -sb[d0 + j], o0, o1);
+                    x[j] = o0;
+                    y[j] = o1;
+                }
+                st(t, g, x);
+                st(t + NT / 2, g, y);
+                continue;
+            }
+            rd(t, g, x);
+            if (rope && d0 < a.rrd) {  // interleaved
+#pragma unroll
+                for (int j = 0; j < 4; j += 2) {
+                    float o0, o1;
+                    rot_pair(x[j], x[j + 1], cb[(d0 + j) / 2], -sb[(d0 + j) / 2], o0, o1);
+                    x[j] = o0;
+                    x[j + 1] = o1;
+                }
+            }
+            st(t, g, x);
         }
 }
 
