@@ -176,7 +176,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         hard_barrier();                                                                                           \
     }
     // sub-step (U, 1): MFMAs on F1, F0 of stage U+1 (NEXT) read one per 3 MFMAs over the first 48, stage U+2's A
-    // pieces into A[SA] (PIECES) one per 4 MFMAs over the first 32 (the A image has one sub-step less to land)
+    // pieces into A[SA] (PIECES) one per 8 MFMAs (one per 4 over the first 32: 0-1.6 % slower,
+    // profiles/gemm_nt_apiece_ab_r4.log)
 #define NT5_SUB1(SA, U, NEXT, PIECES)                                                                             \
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                 if (f_ < 8) fb0[f_] = frag(obn0, f_);                                                             \
                 else fa0[f_ - 8] = frag(oa[(SA) ^ 1][0], f_ - 8);                                                 \
             }                                                                                                     \
-            if ((PIECES) && (m_ & 3) == 3 && m_ < 32) NT_PIECE_AT(false, m_ >> 2, lds0 + (SA) * kImg, (U) + 2)   \
+            if ((PIECES) && (m_ & 7) == 3) NT_PIECE_AT(false, m_ >> 3, lds0 + (SA) * kImg, (U) + 2)              \
         }                                                                                                         \
         NT5_ROTATE()                                                                                              \
     }

@@ -1,4 +1,4 @@
-"""Attention-only driver for kernel profiling (7B shapes): B=2, S=4096, Hq=32, Hkv=8, D=128, causal."""
+"""Attention-only driver for kernel profiling (7B step shapes): B=8 (env B), S=4096, Hq=32, Hkv=8, D=128, causal."""
 import math
 import os
 import sys
@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from scaling_amd.ops import attention  # noqa: E402
 
-B, S, HQ, HK, D = 2, 4096, int(os.environ.get("HQ", 32)), int(os.environ.get("HKV", 8)), 128
+B, S, HQ, HK, D = int(os.environ.get("B", 8)), 4096, int(os.environ.get("HQ", 32)), int(os.environ.get("HKV", 8)), 128
 iters = int(os.environ.get("ITERS", 5))
 T = B * S
 cu = torch.arange(0, T + 1, S, device="cuda", dtype=torch.int32)
@@ -18,21 +18,45 @@ k = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=Tru
 v = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 g = torch.randn(T, HQ, D, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(D)
-for _ in range(2):
-    o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
-    o.backward(g)
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(iters):
-    o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
-torch.cuda.synchronize()
-t1 = time.perf_counter()
-for _ in range(iters):
-    o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
-    o.backward(g)
-torch.cuda.synchronize()
-t2 = time.perf_counter()
-fwd = (t1 - t0) / iters
-tot = (t2 - t1) / iters
-fl = 4 * B * HQ * S * S * D / 2
-print(f"fwd {fwd*1e3:.3f} ms {fl/fwd/1e12:.0f} TF | bwd {(tot-fwd)*1e3:.3f} ms {2.5*fl/(tot-fwd)/1e12:.0f} TF(2.5x)")
+from scaling_amd.ops._ext import ext  # noqa: E402
+
+
+def once():
+    for _ in range(2):
+        o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
+        o.backward(g)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(iters):
+        o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
+        o.backward(g)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    fwd = (t1 - t0) / iters
+    tot = (t2 - t1) / iters
+    fl = 4 * B * HQ * S * S * D / 2
+    return f"fwd {fwd*1e3:.3f} ms {fl/fwd/1e12:.0f} TF | bwd {(tot-fwd)*1e3:.3f} ms {2.5*fl/(tot-fwd)/1e12:.0f} TF(2.5x)"
+
+
+if hasattr(ext(), "fa_set_sched"):  # temporary A/B hook
+    outs = {}
+    for sched in (0, 1, 2):
+        ext().fa_set_sched(sched)
+        qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
+        oo = attention.flash_attention(qq, kk, vv, cu, cu, S, S, sc, True, None)
+        oo.backward(g)
+        outs[sched] = (oo.detach().float(), qq.grad.float(), kk.grad.float(), vv.grad.float())
+    for sched in (1, 2):
+        errs = [((x - y).abs().max() / y.abs().max()).item() for x, y in zip(outs[sched], outs[0])]
+        print(f"sched {sched} vs 0: rel err o/dq/dk/dv {[round(e, 5) for e in errs]}", flush=True)
+    for rnd in range(3):
+        for sched in (0, 1, 2):
+            ext().fa_set_sched(sched)
+            print(f"sched {sched}: {once()}", flush=True)
+    ext().fa_set_sched(1)
+else:
+    print(once())

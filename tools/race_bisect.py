@@ -3,6 +3,7 @@ with every side stream on (multi), every side stream folded (single), and each f
 scaling_amd.core.utils.debug_env.SIDE_STREAM_FEATURES folded alone, and prints (param checksum, loss) per mode.
 
     python tools/race_bisect.py [bench args ...]     (default: --gpus 2, the DP2 case)
+    python tools/race_bisect.py --repeat [bench args ...]   run-to-run determinism, hipBLASLt vs rocBLAS GEMMs
 """
 import json
 import os
@@ -28,7 +29,19 @@ def run(args, env_extra):
 
 
 def main():
-    args = sys.argv[1:] or ["--gpus", "2"]
+    rep = "--repeat" in sys.argv
+    args = [a for a in sys.argv[1:] if a != "--repeat"] or ["--gpus", "2"]
+    if rep:  # run-to-run determinism per GEMM backend, streams folded and not
+        modes = []
+        for tag, env in (("hipblaslt", {}), ("rocblas", {"TORCH_BLAS_PREFER_HIPBLASLT": "0"})):
+            for i in range(2):
+                modes.append((f"single/{tag}#{i}", {**env, "SCALING_AMD_SINGLE_STREAM": "1"}))
+                modes.append((f"multi/{tag}#{i}", dict(env)))
+        out = {}
+        for name, env in modes:
+            out[name] = run(args, env)
+            print(f"{' '.join(args)} | {name:22s} | {out[name]}", flush=True)
+        return
     modes = [("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})]
     for f in ("dp_comm", "opt_step", "wgrad", "tp_comm"):
         modes.append((f"fold:{f}", {"SCALING_AMD_SINGLE_STREAM": f}))
