@@ -156,7 +156,7 @@ __device__ __forceinline__ void store_grad_row(const BwdArgs& a, const f32x16 (&
 // Variants measured against this one and dropped (one wave per SIMD with explicit read-ahead, inline-asm LDS-DMA,
 // paired software-pipelined query tiles): profiles/attn_bwd_variants_ab_r3.log, attn_bwd_pair_ab_r3.log; their code is
 // in git history before commit "Delete losing attention variants".
-template <int D, bool F16, bool DROP, int SCHED = 1>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -245,8 +245,8 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 s = mma<F16>(rd_row<D>(Q, 0, lo.row(ks)), kf[ks], s);
                 dp = mma<F16>(rd_row<D>(DO, 0, lo.row(ks)), rd_row<D>(vw_img, 0, lo.row(ks)), dp);
             }
-            if constexpr (SCHED == 1) {
-            // Q / dO / V row fragments one k-step (3 reads) ahead of their MFMAs (two spill at 256 VGPRs)
+            // Q / dO / V row fragments one k-step (3 reads) ahead of their MFMAs (two spill at 256 VGPRs; the one-per-MFMA
+            // form left every MFMA behind an lgkmcnt(0): 1.5 % slower backward, profiles/attn_sched_ab_r4.log)
             __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
 #pragma unroll
             for (int i = 0; i < NKS - 1; ++i) {
@@ -256,13 +256,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            } else {
-#pragma unroll
-            for (int i = 0; i < 2 * NKS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            }
         }
         // query of register j: qt + 4h + crow(j)
         int mlo = -1 << 30, mhi = 1 << 30;
@@ -313,7 +306,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                     dk[t] = mma<F16>(rd_tr<D>(Q, kb, lo, t), db, dk[t]);
                 }
             }
-            if constexpr (SCHED == 1) {
             // transposed dO / Q fragments one MFMA ahead (two spill at 256 VGPRs)
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
 #pragma unroll
@@ -322,13 +314,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            } else {
-#pragma unroll
-            for (int i = 0; i < 4 * NT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            }
-            }
         }
     };
 
@@ -565,14 +550,12 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
-extern int g_fa_sched;  // TEMPORARY A/B hook (flash_fwd.hip)
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
-        if (D == 128 && g_fa_sched == 0) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP, 0>), grid, 256, lds, st, a);
-        else if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }

@@ -9,7 +9,6 @@
 #include <cstdlib>
 
 #include "flash_attn.h"
-#include <type_traits>
 #include "launch.h"
 
 using namespace sa;
@@ -194,7 +193,7 @@ struct FwdV2 {
 // Variants measured against this one and dropped (8 waves per workgroup, inline-asm LDS-DMA, pinned read-ahead, an
 // 8-wave ping-pong schedule): profiles/attn_fwd_waves_ab_r2.log, attn_fwd_pingpong_ab_r3.log, attn_ab_r2_asyncdma.log;
 // their code is in git history before commit "Delete losing attention variants".
-template <int D, bool F16, bool DROP, int SCHED = 1>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     using C = FwdV2<D>;
@@ -277,22 +276,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
                     s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
-            if constexpr (SCHED == 1) {
-            // K fragment reads kept KPF MFMAs ahead (software pipeline through the sched groups below)
-            constexpr int KPF = 4;
-            __builtin_amdgcn_sched_group_barrier(0x100, KPF, 0);
-#pragma unroll
-            for (int i = 0; i < 2 * C::NKS - KPF; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, KPF, 0);
-            } else {
+            // one K fragment read per MFMA.  Reading them 4 MFMAs ahead (or interleaving the softmax of the previous
+            // tile into these MFMAs) was measured slower: at two waves per SIMD the loop is bound by the SIMD's issue
+            // slots, not by LDS latency (profiles/attn_sched_ab_r4.log)
 #pragma unroll
             for (int i = 0; i < 2 * C::NKS; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            }
             }
         }
         // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
@@ -366,21 +356,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
                         const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
                         o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
                     }
-            if constexpr (SCHED == 1) {
-            constexpr int VPF = 2;  // V^T fragments VPF MFMAs ahead
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * VPF, 1);
-#pragma unroll
-            for (int i = 0; i < 4 * C::NT - VPF; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, VPF, 1);
-            } else {
 #pragma unroll
             for (int i = 0; i < 4 * C::NT; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            }
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
             }
         }
     };
@@ -420,255 +399,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #endif
 }
 
-// ---------------------------------------------------------------------------------------------
-// v3 (D = 64, 128): v2's tiling with the softmax of tile j software-pipelined against the Q K^T of tile j+1
-// (cdna_hip_programming.md T15): per iteration
-//   [vmcnt(0), barrier, LDS-DMA of K_{j+2} and V_{j+1}] -> [row max of S_j, lazy rescale] ->
-//   [Q K_{j+1}^T MFMAs interleaved with exp / row sum / bf16 pack of S_j] -> [mask S_{j+1}] -> [P_j V_j MFMAs]
-// so the exp2 / FMA / add VALU work issues in the MFMA shadow of the next tile's scores instead of between two
-// dependent MFMA phases.  K and V have separate two-slot rings (K_{j+2} may replace K_j once Q K_j^T is done, V_{j+1}
-// may replace V_{j-1} once P_{j-1} V_{j-1} is done), both issued right after the iteration's barrier, so every
-// piece has a whole iteration to land; same 4 x TILE of LDS as v2.
-template <int D, bool F16, bool DROP>
-__global__ __launch_bounds__(256, 2) void fa_fwd_v3_kernel(FwdArgs a) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    using C = FwdV2<D>;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int seg = blockIdx.y, hq = blockIdx.x;
-    const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
-    const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
-    const int ntiles_q = (Lq + C::BM - 1) / C::BM;
-    const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
-    if (qt >= ntiles_q) return;
-    const int hk = hq / (a.Hq / a.Hkv);
-    const int win = hq < a.local_heads ? a.window : -1;
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5,
-              lq = lane & 31;
-    const int off = Lk - Lq;
-    const int qwg0 = qt * C::BM, qw0 = qwg0 + 32 * wave, myq = qw0 + lq;
-    const int qlast = min(qwg0 + C::BM - 1, Lq - 1);
-    int khi = Lk;
-    if (a.causal) khi = min(Lk, qlast + off + 1);
-    else if (win >= 0) khi = min(Lk, qlast + off + win + 1);
-    int klo = 0;
-    if (win >= 0) klo = max(0, qwg0 + off - win);
-    klo = (klo / C::KT) * C::KT;
-
-    int rowoff[C::NKS];
-#pragma unroll
-    for (int ks = 0; ks < C::NKS; ++ks) rowoff[ks] = lds_off<D>(lq, 16 * ks + 8 * h);
-    int troff[C::NT][2];
-    {
-        const int g = (lane >> 4) & 1, i = lane & 15;
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-            troff[t][0] = lds_off<D>(4 * h + (i >> 2), 32 * t + 16 * g + 4 * (i & 3));
-            troff[t][1] = lds_off<D>(4 * h + (i >> 2) + 8, 32 * t + 16 * g + 4 * (i & 3));
-        }
-    }
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    DmaTile<D, C::NW> tk, tv;
-    tk.init(wave_u, lane, a.k_tok);
-    tv.init(wave_u, lane, a.v_tok);
-    const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
-    const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
-    // LDS: K slots 0 / 1 at 0 / TILE, V slots 0 / 1 at 2 TILE / 3 TILE
-#define SA_K_ISSUE(KT, SLOT) dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), smem + (SLOT) * C::TILE, wave_u)
-#define SA_V_ISSUE(KT, SLOT) \
-    dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), smem + (2 + (SLOT)) * C::TILE, wave_u)
-
-    bf16x8 qf[C::NKS];
-    {
-        const u16* qp = a.q + (int64_t)(q0s + min(myq, Lq - 1)) * a.q_tok + (int64_t)hq * a.q_head;
-#pragma unroll
-        for (int ks = 0; ks < C::NKS; ++ks)
-            qf[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u16x8*>(qp + 16 * ks + 8 * h));
-#pragma unroll
-        for (int ks = 0; ks < C::NKS; ++ks) asm volatile("" ::"v"(qf[ks]));
-    }
-    f32x16 o[C::NT];
-#pragma unroll
-    for (int t = 0; t < C::NT; ++t) o[t] = f32x16{};
-    float m = -INFINITY, l = 0.f;
-    const float c2 = a.scale_log2;
-    uint32_t drow = 0;
-    if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
-
-    // S = Q K^T of the tile in K slot KS (no sched groups: callers interleave)
-    auto qk = [&](const char* K, f32x16 (&s)[2]) {
-        s[0] = f32x16{};
-        s[1] = f32x16{};
-#pragma unroll
-        for (int ks = 0; ks < C::NKS; ++ks)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-                s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
-    };
-    auto mask = [&](f32x16 (&s)[2], int kt) {
-        const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
-                               (win >= 0 && (kt < qw0 + 31 + off - win ||
-                                                  (!a.causal && kt + C::KT - 1 > qw0 + off + win)));
-        if (need_mask) {
-            mask_fence();
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int base = kt + 32 * b + 4 * h;
-                int hi = Lk - 1 - base;
-                if (a.causal) hi = min(hi, myq + off - base);
-                else if (win >= 0) hi = min(hi, myq + off + win - base);
-                const int lo = win >= 0 ? myq + off - win - base : -1;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
-            }
-        }
-    };
-    // row max of S and the lazy rescale of O / l
-    auto rowmax = [&](const f32x16 (&s)[2]) {
-        float mx = vmax3(s[0][0], s[0][1], s[0][2]);
-#pragma unroll
-        for (int j = 3; j < 15; j += 2) mx = vmax3(mx, s[0][j], s[0][j + 1]);
-        mx = vmax3(mx, s[0][15], s[1][0]);
-#pragma unroll
-        for (int j = 1; j < 15; j += 2) mx = vmax3(mx, s[1][j], s[1][j + 1]);
-        mx = vmax3(mx, s[1][15], s[1][15]);
-        const float mrow = max_xchg32(mx) * c2;
-        if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {
-            mask_fence();
-            const float mnew = fmaxf(m, mrow);
-            const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
-            l *= alpha;
-#pragma unroll
-            for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) o[t][j] *= alpha;
-            m = mnew;
-        }
-    };
-    // P = exp2(S c - m), row sum into l, dropout, bf16 pack
-    auto softmax = [&](f32x16 (&s)[2], int kt, bf16x8 (&pf)[2][2]) {
-        const float nm = m == -INFINITY ? 0.f : -m;
-        float rs[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
-                s[b][j] = p;
-                rs[j & 3] += p;
-            }
-        l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
-        if constexpr (DROP) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (!drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(j), a.drop_thr)) s[b][j] = 0.f;
-        }
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
-    };
-    auto pv = [&](const char* V, const bf16x8 (&pf)[2][2]) {
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    const int kb = (32 * b + 16 * ss) * D * 2;
-                    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
-                    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
-                    o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
-                }
-        constexpr int VPF = 2;  // V^T fragments VPF MFMAs ahead
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * VPF, 1);
-#pragma unroll
-        for (int i = 0; i < 4 * C::NT - VPF; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, VPF, 1);
-    };
-
-    const int ntiles = khi > klo ? (khi - klo + C::KT - 1) / C::KT : 0;
-    f32x16 sc[2], sn[2];
-    if (ntiles > 0) {
-        SA_K_ISSUE(klo, 0);
-        SA_V_ISSUE(klo, 0);
-        if (ntiles > 1) SA_K_ISSUE(klo + C::KT, 1);
-        // K_0 first: wait for all but the V_0 / K_1 pieces would need exact counts per wave; the prologue waits for all
-        __syncthreads();
-        qk(smem, sc);
-        mask(sc, klo);
-    }
-    // iteration j (parity P = j & 1): K_{j+1} in K slot P^1, V_j in V slot P; K_{j+2} -> K slot P, V_{j+1} -> V slot P^1
-    auto iter = [&](auto PAR, int j) {
-        constexpr int P = decltype(PAR)::value;
-        const int kt = klo + j * C::KT;
-        __syncthreads();  // (vmcnt(0) + barrier) K_{j+1}, V_j landed; K slot P and V slot P^1 free
-        if (j + 2 < ntiles) SA_K_ISSUE(kt + 2 * C::KT, P);
-        if (j + 1 < ntiles) SA_V_ISSUE(kt + C::KT, P ^ 1);
-        rowmax(sc);
-        bf16x8 pf[2][2];
-        if (j + 1 < ntiles) {
-            qk(smem + (P ^ 1) * C::TILE, sn);
-            softmax(sc, kt, pf);
-            // Q K_{j+1}^T: K fragments 4 MFMAs ahead, the exp / sum / pack VALU of S_j spread over the MFMA gaps
-            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-            for (int i = 0; i < 2 * C::NKS - 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-            }
-            mask(sn, kt + C::KT);
-        } else {
-            softmax(sc, kt, pf);
-        }
-        pv(smem + (2 + P) * C::TILE, pf);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) sc[b] = sn[b];
-    };
-    int j = 0;
-    for (; j + 1 < ntiles; j += 2) {
-        iter(std::integral_constant<int, 0>{}, j);
-        iter(std::integral_constant<int, 1>{}, j + 1);
-    }
-    if (j < ntiles) iter(std::integral_constant<int, 0>{}, j);
-#undef SA_K_ISSUE
-#undef SA_V_ISSUE
-    if (myq < Lq) {
-        const float inv = (l > 0.f ? 1.f / l : 0.f) * (DROP ? a.rp_drop : 1.f);
-        u16* op = a.o + (int64_t)(q0s + myq) * a.o_tok + (int64_t)hq * a.o_head;
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                u16x4 w;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) w[jj] = f2t<F16>(o[t][4 * g + jj] * inv);
-                *reinterpret_cast<u16x4*>(op + 32 * t + 8 * g + 4 * h) = w;
-            }
-        if (h == 0)
-            a.lse[(int64_t)hq * a.lse_stride + q0s + myq] = l > 0.f ? (m + __log2f(l)) * 0.69314718055994530942f : INFINITY;
-    }
-#endif
-}
-
-int g_fa_sched = 1;  // TEMPORARY A/B hook: 0 = previous fragment-read schedule
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
         dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(256);
-        if (D == 128 && g_fa_sched == 0) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, 0>), grid, block, 4 * FwdV2<128>::TILE, st, a);
-        else if (D == 128 && g_fa_sched == 2) hipLaunchKernelGGL((fa_fwd_v3_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
-        else if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
         else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
         return;
     }
@@ -677,7 +412,6 @@ static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
 }
 
 namespace sa_launch {
-void fa_set_sched(int v) { g_fa_sched = v; }
 void fa_fwd(const FwdArgs& a, int D, int max_q, bool f16, hipStream_t st) {
     const bool drop = a.p_drop > 0.f;
     if (f16) {

@@ -127,6 +127,10 @@ class Topology:
             if backend == "nccl":
                 kwargs["device_id"] = self.device
             dist.init_process_group(**kwargs)
+        if backend == "gloo" and self.device.type == "cuda":  # 1-GPU rehearsal: make gloo stream-ordered
+            from .gloo_gpu import install
+
+            install()
         # every rank creates every group in the same order (collective requirement)
         for ranks in self.all_pipe_parallel_groups:
             g = dist.new_group(ranks)

@@ -1,0 +1,54 @@
+"""The rehearsal's host-staged collectives (scaling_amd/core/topology/gloo_gpu.py) return what the plain gloo
+collectives return (here on CPU ranks, with the device-tensor test forced on so the staging path runs)."""
+import os
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from scaling_amd.core.utils.port import find_free_port
+
+
+def _worker(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from scaling_amd.core.topology import gloo_gpu
+
+    gloo_gpu._cuda = lambda t: isinstance(t, torch.Tensor)  # every tensor takes the staged path
+    gloo_gpu.install()
+    x = torch.arange(8, dtype=torch.float32) + 10 * rank
+    a = x.clone()
+    w = dist.all_reduce(a, async_op=True)
+    assert w.wait()
+    rs = torch.empty(4)
+    dist.reduce_scatter_tensor(rs, x.clone())
+    ag = torch.empty(16)
+    dist.all_gather_into_tensor(ag, x[:8:1].clone())
+    bc = x.clone()
+    dist.broadcast(bc, src=1)
+    lst = [torch.empty(8) for _ in range(world)]
+    dist.all_gather(lst, x)
+    q.put((rank, a, rs, ag, bc, torch.stack(lst)))
+    dist.destroy_process_group()
+
+
+def test_host_staged_collectives_match_gloo():
+    world, port = 2, find_free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    xs = [torch.arange(8, dtype=torch.float32) + 10 * r for r in range(world)]
+    tot = xs[0] + xs[1]
+    for r in range(world):
+        a, rs, ag, bc, lst = res[r]
+        assert torch.equal(a, tot)
+        assert torch.equal(rs, tot[4 * r: 4 * r + 4])
+        assert torch.equal(ag, torch.cat(xs))
+        assert torch.equal(bc, xs[1])
+        assert torch.equal(lst, torch.stack(xs))

@@ -18,8 +18,6 @@ k = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=Tru
 v = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 g = torch.randn(T, HQ, D, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(D)
-from scaling_amd.ops._ext import ext  # noqa: E402
-
 
 def once():
     for _ in range(2):
@@ -42,21 +40,5 @@ def once():
     return f"fwd {fwd*1e3:.3f} ms {fl/fwd/1e12:.0f} TF | bwd {(tot-fwd)*1e3:.3f} ms {2.5*fl/(tot-fwd)/1e12:.0f} TF(2.5x)"
 
 
-if hasattr(ext(), "fa_set_sched"):  # temporary A/B hook
-    outs = {}
-    for sched in (0, 1, 2):
-        ext().fa_set_sched(sched)
-        qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
-        oo = attention.flash_attention(qq, kk, vv, cu, cu, S, S, sc, True, None)
-        oo.backward(g)
-        outs[sched] = (oo.detach().float(), qq.grad.float(), kk.grad.float(), vv.grad.float())
-    for sched in (1, 2):
-        errs = [((x - y).abs().max() / y.abs().max()).item() for x, y in zip(outs[sched], outs[0])]
-        print(f"sched {sched} vs 0: rel err o/dq/dk/dv {[round(e, 5) for e in errs]}", flush=True)
-    for rnd in range(3):
-        for sched in (0, 1, 2):
-            ext().fa_set_sched(sched)
-            print(f"sched {sched}: {once()}", flush=True)
-    ext().fa_set_sched(1)
-else:
-    print(once())
+for _ in range(3):
+    print(once(), flush=True)
