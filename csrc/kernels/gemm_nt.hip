@@ -115,6 +115,23 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                          "v"(va), "s"(rsa), "s"(abase + (I) * astep + ku_)                                         \
                          : "m0");                                                                                 \
     }
+    // in the loop: the piece together with the MFMA before it, in one statement -- the MFMA is the wait state between
+    // the M0 write and the LDS-DMA instead of an s_nop issue slot (+1.6-3 %, profiles/gemm_nt_mfma_piece_ab_r4.log)
+#define NT_MFMA_PIECE_AT(C_, A_, B_, ISB, I, LBASE, U)                                                              \
+    {                                                                                                             \
+        const uint32_t l_ = (LBASE) + (wave + 4 * (I)) * 1024;                                                    \
+        const int ku_ = (U) * 128;                                                                                \
+        if (ISB)                                                                                                  \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                      \
+                         "buffer_load_dwordx4 %4, %5, %6 offen lds"                                               \
+                         : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(vb), "s"(rsb),                               \
+                           "s"(bbase + (I) * bstep + ku_) : "m0");                                                 \
+        else                                                                                                      \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                      \
+                         "buffer_load_dwordx4 %4, %5, %6 offen lds"                                               \
+                         : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(va), "s"(rsa),                               \
+                           "s"(abase + (I) * astep + ku_) : "m0");                                                 \
+    }
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -161,14 +178,14 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
 #define NT5_SUB0(SA, U, PIECES)                                                                                   \
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
-            mfma(acc[i][j], fb0[j], fa0[i]);                                                                      \
             const int m_ = i * 8 + j;                                                                             \
+            if ((PIECES) && (m_ & 7) == 7) NT_MFMA_PIECE_AT(acc[i][j], fb0[j], fa0[i], true, m_ >> 3, lbnn, (U) + 2) \
+            else mfma(acc[i][j], fb0[j], fa0[i]);                                                                 \
             if (m_ % 3 == 1 && m_ < 48) {                                                                         \
                 const int f_ = m_ / 3;                                                                            \
                 if (f_ < 8) fb1[f_] = frag(obc1, f_);                                                             \
                 else fa1[f_ - 8] = frag(oa[SA][1], f_ - 8);                                                       \
             }                                                                                                     \
-            if ((PIECES) && (m_ & 7) == 7) NT_PIECE_AT(true, m_ >> 3, lbnn, (U) + 2)                            \
         }                                                                                                         \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                        \
         if (PIECES) wait_vm<8>();                                                                                 \
@@ -181,14 +198,15 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
 #define NT5_SUB1(SA, U, NEXT, PIECES)                                                                             \
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
-            mfma(acc[i][j], fb1[j], fa1[i]);                                                                      \
             const int m_ = i * 8 + j;                                                                             \
+            if ((PIECES) && (m_ & 7) == 3)                                                                        \
+                NT_MFMA_PIECE_AT(acc[i][j], fb1[j], fa1[i], false, m_ >> 3, lds0 + (SA) * kImg, (U) + 2)          \
+            else mfma(acc[i][j], fb1[j], fa1[i]);                                                                 \
             if ((NEXT) && m_ % 3 == 1 && m_ < 48) {                                                               \
                 const int f_ = m_ / 3;                                                                            \
                 if (f_ < 8) fb0[f_] = frag(obn0, f_);                                                             \
                 else fa0[f_ - 8] = frag(oa[(SA) ^ 1][0], f_ - 8);                                                 \
             }                                                                                                     \
-            if ((PIECES) && (m_ & 7) == 3) NT_PIECE_AT(false, m_ >> 3, lds0 + (SA) * kImg, (U) + 2)              \
         }                                                                                                         \
         NT5_ROTATE()                                                                                              \
     }
@@ -228,6 +246,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
 #undef NT5_SUB1
 #undef NT5_ROTATE
 #undef NT_PIECE_AT
+#undef NT_MFMA_PIECE_AT
     wait_vm<0>();
     // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
     // and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without it hipcc hoists

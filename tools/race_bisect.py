@@ -3,7 +3,7 @@ with every side stream on (multi), every side stream folded (single), and each f
 scaling_amd.core.utils.debug_env.SIDE_STREAM_FEATURES folded alone, and prints (param checksum, loss) per mode.
 
     python tools/race_bisect.py [bench args ...]     (default: --gpus 2, the DP2 case)
-    python tools/race_bisect.py --repeat [bench args ...]   run-to-run determinism, hipBLASLt vs rocBLAS GEMMs
+    python tools/race_bisect.py --repeat [bench args ...]   run-to-run determinism (single stream) per GEMM setting
 """
 import json
 import os
@@ -33,10 +33,12 @@ def main():
     args = [a for a in sys.argv[1:] if a != "--repeat"] or ["--gpus", "2"]
     if rep:  # run-to-run determinism per GEMM backend, streams folded and not
         modes = []
-        for tag, env in (("hipblaslt", {}), ("rocblas", {"TORCH_BLAS_PREFER_HIPBLASLT": "0"})):
+        variants = (("default", {}), ("sk-static", {"TENSILE_STREAMK_DYNAMIC_GRID": "0"}),
+                    ("tunable-off", {"SCALING_AMD_GEMM_TUNING": "off"}),
+                    ("rocblas", {"SCALING_AMD_GEMM_TUNING": "off", "TORCH_BLAS_PREFER_HIPBLASLT": "0"}))
+        for tag, env in variants:
             for i in range(2):
                 modes.append((f"single/{tag}#{i}", {**env, "SCALING_AMD_SINGLE_STREAM": "1"}))
-                modes.append((f"multi/{tag}#{i}", dict(env)))
         out = {}
         for name, env in modes:
             out[name] = run(args, env)
