@@ -128,6 +128,24 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
                          "v"(voff_a), "s"(rsa), "s"((SA) + i_ * step_a)                                       \
                          : "m0");                                                                                \
     }
+    // in the loop: the piece in one statement with the MFMA before it -- the MFMA is the wait state between the M0
+    // write and the LDS-DMA, where an s_nop would take an issue slot (the same change gained 1.6-3 % on the NT kernel,
+    // profiles/gemm_nt_mfma_piece_ab_r4.log)
+#define SA_RING_MFMA_PIECE(C_, A_, B_, P, SLOT, SA, SB)                                                          \
+    {                                                                                                            \
+        const int i_ = (P) >> 1;                                                                                 \
+        const uint32_t l_ = lds0 + (SLOT) * kSlot + (((P) & 1) ? kImg : 0) + (wave + NW * i_) * 1024;            \
+        if ((P) & 1)                                                                                             \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                     \
+                         "buffer_load_dwordx4 %4, %5, %6 offen lds"                                              \
+                         : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(voff_b), "s"(rsb), "s"((SB) + i_ * step_b)  \
+                         : "m0");                                                                                \
+        else                                                                                                     \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                     \
+                         "buffer_load_dwordx4 %4, %5, %6 offen lds"                                              \
+                         : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(voff_a), "s"(rsa), "s"((SA) + i_ * step_a)  \
+                         : "m0");                                                                                \
+    }
 
     f32x4 acc[8][8];
 #pragma unroll
@@ -168,10 +186,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
         const int sa_ = soff_a((T) + 4), sb_ = soff_b((T) + 4);                                                 \
         _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
             _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                     \
-                mfma16_acc(acc[i][j], FB[j], FA[i]);                                                            \
                 const int m_ = i * 8 + j;                                                                       \
+                if ((m_ & 7) == 3) SA_RING_MFMA_PIECE(acc[i][j], FB[j], FA[i], m_ >> 3, SLOT, sa_, sb_)         \
+                else mfma16_acc(acc[i][j], FB[j], FA[i]);                                                       \
                 if ((m_ & 3) == 1) SA_RING_READ(((SLOT) + 1) & 3, NA, NB, m_ >> 2)                              \
-                if ((m_ & 7) == 3) SA_RING_PIECE(m_ >> 3, SLOT, sa_, sb_)                                       \
             }                                                                                                   \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
         wait_vm<4 * NP>();                                                                                      \
@@ -204,6 +222,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
 #undef SA_RING_STEP
 #undef SA_RING_READ
 #undef SA_RING_PIECE
+#undef SA_RING_MFMA_PIECE
     wait_vm<0>();
     // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
     // and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without it hipcc hoists

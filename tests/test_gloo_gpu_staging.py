@@ -20,9 +20,9 @@ def _worker(rank: int, world: int, port: int, q) -> None:
     a = x.clone()
     w = dist.all_reduce(a, async_op=True)
     assert w.wait()
-    rs = torch.empty(4)
+    rs = torch.empty(8 // world)
     dist.reduce_scatter_tensor(rs, x.clone())
-    ag = torch.empty(16)
+    ag = torch.empty(8 * world)
     dist.all_gather_into_tensor(ag, x[:8:1].clone())
     bc = x.clone()
     dist.broadcast(bc, src=1)
@@ -32,8 +32,12 @@ def _worker(rank: int, world: int, port: int, q) -> None:
     dist.destroy_process_group()
 
 
-def test_host_staged_collectives_match_gloo():
-    world, port = 2, find_free_port()
+import pytest
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_host_staged_collectives_match_gloo(world):
+    port = find_free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -44,11 +48,12 @@ def test_host_staged_collectives_match_gloo():
         p.join(60)
         assert p.exitcode == 0
     xs = [torch.arange(8, dtype=torch.float32) + 10 * r for r in range(world)]
-    tot = xs[0] + xs[1]
+    tot = sum(xs[1:], xs[0].clone())
+    per = 8 // world
     for r in range(world):
         a, rs, ag, bc, lst = res[r]
         assert torch.equal(a, tot)
-        assert torch.equal(rs, tot[4 * r: 4 * r + 4])
+        assert torch.equal(rs, tot[per * r: per * (r + 1)])
         assert torch.equal(ag, torch.cat(xs))
         assert torch.equal(bc, xs[1])
         assert torch.equal(lst, torch.stack(xs))
