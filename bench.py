@@ -307,10 +307,22 @@ def _worker(a: argparse.Namespace) -> None:
         if dev.type == "cuda":
             torch.cuda.synchronize()
 
+    trace = os.environ.get("SCALING_AMD_BENCH_TRACE")  # race-check forensics: per-step values per rank (JSON lines)
+    n_steps = [0]
+
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,
                                metrics_aggregation_fn)
         context.step()
+        if trace:
+            optimizer.wait_param_sync()
+            with torch.no_grad():
+                rec = {"step": n_steps[0], "loss": out.loss, "grad_norm": out.global_grad_norm,
+                       "params": [float(p.detach().double().sum()) for p in model.parameters()],
+                       "grads": [float(g.grad_source().double().sum()) for g in optimizer.parameter_groups]}
+            with open(f"{trace}.rank{rank}.jsonl", "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        n_steps[0] += 1
         return out
 
     for _ in range(a.warmup):

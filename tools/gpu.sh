@@ -12,6 +12,7 @@
 #   decode     tools/decode_bench.py
 #   race       the multi- vs single-stream race check (tests/test_gpu_rehearsal.py -k race_check)
 #   race_bisect  tools/race_bisect.py: which side stream makes a layout differ from its single-stream twin
+#   race_trace   tools/race_trace.py: the first step / quantity where two identical runs differ
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -52,6 +53,8 @@ for step in "$@"; do
             -k "race_check" > gpurun_out/race_$TAG.log 2>&1 ;;
     race_bisect)
         $T 900 $PY tools/race_bisect.py ${RACE_ARGS:-} > gpurun_out/race_bisect_$TAG.log 2>&1 ;;
+    race_trace)
+        $T 600 $PY tools/race_trace.py ${RACE_ARGS:-} > gpurun_out/race_trace_$TAG.log 2>&1 ;;
     *)
         echo "unknown step $step"; exit 2 ;;
     esac

@@ -1,0 +1,68 @@
+"""Forensics for a run-to-run difference of the race check: runs one bench layout twice (same settings, by default
+DP2 with every side stream folded) with SCALING_AMD_BENCH_TRACE, then reports the first step and quantity where the
+two runs differ per rank: the loss (forward of that step), the reduced gradients (backward + DP reduction) or a
+parameter (optimizer update).
+
+    python tools/race_trace.py [bench args ...]      (default: --gpus 2)
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BASE = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
+        "--warmup", "1"]
+
+
+def run(args, prefix, env_extra):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.update(env_extra)
+    env["SCALING_AMD_BENCH_TRACE"] = prefix
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *BASE, *args], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        print(r.stderr[-3000:])
+        raise SystemExit(1)
+
+
+def load(prefix, rank):
+    with open(f"{prefix}.rank{rank}.jsonl") as f:
+        return [json.loads(x) for x in f]
+
+
+def main():
+    args = sys.argv[1:] or ["--gpus", "2"]
+    gpus = int(args[args.index("--gpus") + 1]) if "--gpus" in args else 1
+    out = os.path.join(ROOT, "gpurun_out", "race_trace")
+    os.makedirs(out, exist_ok=True)
+    env = {"SCALING_AMD_SINGLE_STREAM": os.environ.get("SCALING_AMD_SINGLE_STREAM", "1")}
+    for i in range(2):
+        for r in range(gpus):
+            p = os.path.join(out, f"run{i}.rank{r}.jsonl")
+            if os.path.exists(p):
+                os.remove(p)
+        run(args, os.path.join(out, f"run{i}"), env)
+    for r in range(gpus):
+        a, b = load(os.path.join(out, "run0"), r), load(os.path.join(out, "run1"), r)
+        first = None
+        for x, y in zip(a, b):
+            for key in ("loss", "grads", "grad_norm", "params"):
+                if x[key] != y[key]:
+                    diff = key
+                    if isinstance(x[key], list):
+                        idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
+                        diff = f"{key} (indices {idx[:8]}{'...' if len(idx) > 8 else ''} of {len(x[key])})"
+                    first = (x["step"], diff, x["loss"], y["loss"])
+                    break
+            if first:
+                break
+        print(f"rank {r}: " + ("identical" if first is None else
+                               f"first difference at step {first[0]}: {first[1]} (loss {first[2]} vs {first[3]})"),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
