@@ -318,8 +318,12 @@ def _worker(a: argparse.Namespace) -> None:
             optimizer.wait_param_sync()
             with torch.no_grad():
                 rec = {"step": n_steps[0], "loss": out.loss, "grad_norm": out.global_grad_norm,
+                       "names": [n for n, _ in model.named_parameters()] if n_steps[0] == 0 else None,
                        "params": [float(p.detach().double().sum()) for p in model.parameters()],
-                       "grads": [float(g.grad_source().double().sum()) for g in optimizer.parameter_groups]}
+                       "grads": [float(g.grad_source().double().sum()) for g in optimizer.parameter_groups],
+                       # local (pre-reduction) gradients: lazy zeroing leaves them in the flat buffer after the step
+                       "pgrads": [float(p.grad.double().sum()) if p.grad is not None else None
+                                  for p in model.parameters()]}
             with open(f"{trace}.rank{rank}.jsonl", "a") as f:
                 f.write(json.dumps(rec) + "\n")
         n_steps[0] += 1

@@ -149,6 +149,23 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
     asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// max of 16 floats as ONE statement of 8 dependent v_max3: hipcc pads every inline-asm boundary whose output the next
+// VALU reads with an s_nop, so 16 single-instruction vmax3 statements cost 16 extra issue slots per row max
+__device__ __forceinline__ float vmax16(const f32x16& x) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3\n\t"
+        "v_max3_f32 %0, %0, %4, %5\n\t"
+        "v_max3_f32 %0, %0, %6, %7\n\t"
+        "v_max3_f32 %0, %0, %8, %9\n\t"
+        "v_max3_f32 %0, %0, %10, %11\n\t"
+        "v_max3_f32 %0, %0, %12, %13\n\t"
+        "v_max3_f32 %0, %0, %14, %15\n\t"
+        "v_max_f32 %0, %0, %16"
+        : "=&v"(r)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]),
+          "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14]), "v"(x[15]));
+    return r;
+}
 // lane l and lane l^32 combined with one v_permlane32_swap: returns {x_l, x_(l^32)} in some order
 __device__ __forceinline__ void xchg32(float x, float& a, float& b) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);

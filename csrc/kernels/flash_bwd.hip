@@ -86,19 +86,12 @@ __device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffs
 // rope kernel on the rounded gradient (round, rotate with rot_pair and sign -1, round), so the fold is bit-identical
 // to flash backward + rope(..., inverse).  NeoX (full rotation, rrd == D: the binding checks) pairs dims d, d + D/2 =
 // accumulators t and t + NT/2 of the same lane; interleaved pairs are elements (2p, 2p+1) of one 4-element group.
-// One 4-element group (two for a NeoX pair) is live at a time: the epilogue must not raise the kernel's register peak.
+// Only wave-uniform branches, and the row's cos / sin loads are issued together before the first use (a branch per
+// group exposed one global-load latency per group: +2.8 ms/step of dQ epilogue, profiles/rocprof_7b_r4j_step.md).
 template <int D, bool F16>
 __device__ __forceinline__ void store_grad_row(const BwdArgs& a, const f32x16 (&acc)[D / 32], float scale, int64_t tok,
                                                int h, u16* dst) {
     constexpr int NT = D / 32;
-    const bool rope = a.rcos != nullptr;
-    const float* cb = nullptr;
-    const float* sb = nullptr;
-    if (rope) {
-        const int64_t ps = a.rpos ? a.rpos[tok] : (tok % a.rseq);
-        cb = a.rcos + ps * (a.rrd / 2);
-        sb = a.rsin + ps * (a.rrd / 2);
-    }
     auto rd = [&](int t, int g, float (&x)[4]) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[j] = t2f<F16>(f2t<F16>(acc[t][4 * g + j] * scale));
@@ -109,38 +102,74 @@ __device__ __forceinline__ void store_grad_row(const BwdArgs& a, const f32x16 (&
         for (int j = 0; j < 4; ++j) w[j] = f2t<F16>(x[j]);
         *reinterpret_cast<u16x4*>(dst + 32 * t + 8 * g + 4 * h) = w;
     };
+    if (a.rcos == nullptr) {  // wave-uniform branches only; the table loads of a rotating row are all issued up front
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int d0 = 32 * t + 8 * g + 4 * h;
-            float x[4];
-            if (rope && !a.ril) {  // NeoX, rrd == D
-                if (t >= NT / 2) continue;  // stored with its partner
-                float y[4];
+            for (int g = 0; g < 4; ++g) {
+                float x[4];
+                rd(t, g, x);
+                st(t, g, x);
+            }
+        return;
+    }
+    const int64_t ps = a.rpos ? a.rpos[tok] : (tok % a.rseq);
+    const float* cb = a.rcos + ps * (a.rrd / 2);
+    const float* sb = a.rsin + ps * (a.rrd / 2);
+    if constexpr (NT < 2) return;  // D = 32: never folded (fa_bwd binding)
+    if (!a.ril) {  // NeoX, rrd == D: dims d (acc t < NT/2) and d + D/2 (acc t + NT/2) share cos / sin [d]
+        constexpr int NH = NT / 2 > 0 ? NT / 2 : 1;
+        f32x4 cv[NH][4], sv[NH][4];
+#pragma unroll
+        for (int t = 0; t < NT / 2; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                cv[t][g] = *reinterpret_cast<const f32x4*>(cb + 32 * t + 8 * g + 4 * h);
+                sv[t][g] = *reinterpret_cast<const f32x4*>(sb + 32 * t + 8 * g + 4 * h);
+            }
+#pragma unroll
+        for (int t = 0; t < NT / 2; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float x[4], y[4];
                 rd(t, g, x);
                 rd(t + NT / 2, g, y);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     float o0, o1;
-                    rot_pair(x[j], y[j], cb[d0 + j], -sb[d0 + j], o0, o1);
+                    rot_pair(x[j], y[j], cv[t][g][j], -sv[t][g][j], o0, o1);
                     x[j] = o0;
                     y[j] = o1;
                 }
                 st(t, g, x);
                 st(t + NT / 2, g, y);
-                continue;
             }
-            rd(t, g, x);
-            if (rope && d0 < a.rrd) {  // interleaved
+        return;
+    }
+    // interleaved: elements (2p, 2p+1) of a 4-element group are pair p = d/2 of dims below rrd; cos / sin pairs of
+    // dims past rrd are read clamped and the rotation is discarded by a select
+    const int hr = a.rrd / 2 - 2;
+    float2 cv[NT][4], sv[NT][4];
 #pragma unroll
-                for (int j = 0; j < 4; j += 2) {
-                    float o0, o1;
-                    rot_pair(x[j], x[j + 1], cb[(d0 + j) / 2], -sb[(d0 + j) / 2], o0, o1);
-                    x[j] = o0;
-                    x[j + 1] = o1;
-                }
-            }
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int p = min((32 * t + 8 * g + 4 * h) / 2, hr);
+            cv[t][g] = *reinterpret_cast<const float2*>(cb + p);
+            sv[t][g] = *reinterpret_cast<const float2*>(sb + p);
+        }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const bool rot = 32 * t + 8 * g + 4 * h < a.rrd;
+            float x[4];
+            rd(t, g, x);
+            float o[4];
+            rot_pair(x[0], x[1], cv[t][g].x, -sv[t][g].x, o[0], o[1]);
+            rot_pair(x[2], x[3], cv[t][g].y, -sv[t][g].y, o[2], o[3]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = rot ? o[j] : x[j];
             st(t, g, x);
         }
 }

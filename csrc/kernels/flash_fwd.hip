@@ -302,13 +302,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
                 for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
             }
         }
-        float mx = vmax3(s[0][0], s[0][1], s[0][2]);
-#pragma unroll
-        for (int j = 3; j < 15; j += 2) mx = vmax3(mx, s[0][j], s[0][j + 1]);
-        mx = vmax3(mx, s[0][15], s[1][0]);
-#pragma unroll
-        for (int j = 1; j < 15; j += 2) mx = vmax3(mx, s[1][j], s[1][j + 1]);
-        mx = vmax3(mx, s[1][15], s[1][15]);
+        // two independent 16-element chains, one statement each (no hazard pads inside)
+        const float m0 = vmax16(s[0]), m1 = vmax16(s[1]);
+        const float mx = vmax3(m0, m1, m1);
         const float mrow = max_xchg32(mx) * c2;
         if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {  // rare after the first tiles
             mask_fence();
@@ -322,16 +318,16 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
             m = mnew;
         }
         const float nm = m == -INFINITY ? 0.f : -m;
-        float rs = 0.f;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
                 s[b][j] = p;
-                rs += p;
+                rs[j & 3] += p;
             }
-        l += sum_xchg32(rs);
+        l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
         if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
 #pragma unroll
             for (int b = 0; b < 2; ++b)

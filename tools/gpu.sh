@@ -33,7 +33,7 @@ for step in "$@"; do
     prof)
         (cd /tmp && export TMPDIR=/tmp && $T 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run \
             -- python3 "$R/bench.py" ${PROF_ARGS:---steps 3 --warmup 1} > "$R/gpurun_out/prof_$TAG.log" 2>&1)
-        $PY tools/rocpd_step.py gpurun_out/prof_$TAG > gpurun_out/prof_step_$TAG.md 2>&1 || true ;;
+        $PY tools/rocpd_step.py gpurun_out/prof_$TAG/run_results.db > gpurun_out/prof_step_$TAG.md 2>&1 || true ;;
     pmc)
         B="$R/bench.py ${PMC_ARGS:---steps 1 --warmup 1 --num-layers 4}"
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
