@@ -285,6 +285,11 @@ def _worker(a: argparse.Namespace) -> None:
     from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
 
     gpu = a.backend != "gloo"
+    if os.environ.get("SCALING_AMD_DETERMINISTIC") == "1":  # library-side determinism (race-check forensics)
+        from scaling_amd.core.utils.debug_env import DETERMINISTIC_ENV, apply
+
+        apply(DETERMINISTIC_ENV)
+        torch.use_deterministic_algorithms(True)
     gemm_mode = enable_tuned_gemms(a.gemm_tuning, a.gemm_tuning_out, rank) if gpu else "off"
     cfg_dict = _config_dict(a, world, rank, local)
     arch = cfg_dict["transformer_architecture"]

@@ -33,9 +33,12 @@ def main():
     args = [a for a in sys.argv[1:] if a != "--repeat"] or ["--gpus", "2"]
     if rep:  # run-to-run determinism per GEMM backend, streams folded and not
         modes = []
-        variants = (("default", {}), ("sk-static", {"TENSILE_STREAMK_DYNAMIC_GRID": "0"}),
-                    ("tunable-off", {"SCALING_AMD_GEMM_TUNING": "off"}),
-                    ("rocblas", {"SCALING_AMD_GEMM_TUNING": "off", "TORCH_BLAS_PREFER_HIPBLASLT": "0"}))
+        variants = (("default", {}),
+                    ("rocblas-noatomics", {"SCALING_AMD_GEMM_TUNING": "off", "TORCH_BLAS_PREFER_HIPBLASLT": "0",
+                                           "ROCBLAS_DEFAULT_ATOMICS_MODE": "0"}),
+                    ("torch-deterministic", {"SCALING_AMD_DETERMINISTIC": "1"}),
+                    ("rocblas-deterministic", {"SCALING_AMD_DETERMINISTIC": "1", "SCALING_AMD_GEMM_TUNING": "off",
+                                               "TORCH_BLAS_PREFER_HIPBLASLT": "0"}))
         for tag, env in variants:
             for i in range(2):
                 modes.append((f"single/{tag}#{i}", {**env, "SCALING_AMD_SINGLE_STREAM": "1"}))
