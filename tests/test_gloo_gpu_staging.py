@@ -28,7 +28,8 @@ def _worker(rank: int, world: int, port: int, q) -> None:
     dist.broadcast(bc, src=1)
     lst = [torch.empty(8) for _ in range(world)]
     dist.all_gather(lst, x)
-    q.put((rank, a, rs, ag, bc, torch.stack(lst)))
+    # plain lists: a tensor on the queue travels by file descriptor, which dies with this process
+    q.put((rank, a.tolist(), rs.tolist(), ag.tolist(), bc.tolist(), torch.stack(lst).tolist()))
     dist.destroy_process_group()
 
 
@@ -51,7 +52,7 @@ def test_host_staged_collectives_match_gloo(world):
     tot = sum(xs[1:], xs[0].clone())
     per = 8 // world
     for r in range(world):
-        a, rs, ag, bc, lst = res[r]
+        a, rs, ag, bc, lst = (torch.tensor(v) for v in res[r])
         assert torch.equal(a, tot)
         assert torch.equal(rs, tot[per * r: per * (r + 1)])
         assert torch.equal(ag, torch.cat(xs))

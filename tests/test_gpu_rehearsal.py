@@ -116,12 +116,15 @@ def test_race_check_multi_stream_equals_single_stream(args, env):
     """Race check: the multi-stream schedule (DP communication stream, overlapped optimizer step,
     optional weight-gradient stream, per-layer event waits) must leave bit-identical parameters and losses to
     the same run with every side stream folded onto the compute stream (SCALING_AMD_SINGLE_STREAM=1).  A missing
-    stream / event dependency shows up as a different checksum."""
+    stream / event dependency shows up as a different checksum.  Both runs use library-side determinism
+    (SCALING_AMD_DETERMINISTIC=1: torch deterministic algorithms, rocBLAS without atomics): with several ranks sharing
+    the one GPU, the default vendor GEMM kernels' atomic accumulation order varies from run to run even with every
+    stream folded (profiles/race_repeat_dp2_r4.log), which would hide what this test checks."""
     base = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
             "--warmup", "1"]
     out = {}
     for mode, extra in (("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})):
-        r = _run([*base, *args], env_extra={**env, **extra}, timeout=300)
+        r = _run([*base, *args], env_extra={**env, **extra, "SCALING_AMD_DETERMINISTIC": "1"}, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
         res = _json_lines(r.stdout)[0]["config"]
         out[mode] = (res["param_checksum"], res["loss"])

@@ -47,10 +47,11 @@ def main():
             out[name] = run(args, env)
             print(f"{' '.join(args)} | {name:22s} | {out[name]}", flush=True)
         return
-    modes = [("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})]
+    det = {"SCALING_AMD_DETERMINISTIC": "1"}  # as the race-check test: vendor kernels deterministic
+    modes = [("multi", dict(det)), ("single", {**det, "SCALING_AMD_SINGLE_STREAM": "1"})]
     for f in ("dp_comm", "opt_step", "wgrad", "tp_comm"):
-        modes.append((f"fold:{f}", {"SCALING_AMD_SINGLE_STREAM": f}))
-    modes.append(("multi-again", {}))
+        modes.append((f"fold:{f}", {**det, "SCALING_AMD_SINGLE_STREAM": f}))
+    modes.append(("multi-again", dict(det)))
     out = {}
     for name, env in modes:
         out[name] = run(args, env)
