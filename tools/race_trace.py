@@ -38,33 +38,35 @@ def main():
     gpus = int(args[args.index("--gpus") + 1]) if "--gpus" in args else 1
     out = os.path.join(ROOT, "gpurun_out", "race_trace")
     os.makedirs(out, exist_ok=True)
-    env = {"SCALING_AMD_SINGLE_STREAM": os.environ.get("SCALING_AMD_SINGLE_STREAM", "1")}
-    for i in range(2):
+    env = {"SCALING_AMD_SINGLE_STREAM": os.environ.get("SCALING_AMD_SINGLE_STREAM", "1"),
+           "SCALING_AMD_DETERMINISTIC": "1"}
+    runs = int(os.environ.get("RACE_TRACE_RUNS", "2"))
+    for i in range(runs):
         for r in range(gpus):
             p = os.path.join(out, f"run{i}.rank{r}.jsonl")
             if os.path.exists(p):
                 os.remove(p)
         run(args, os.path.join(out, f"run{i}"), env)
-    for r in range(gpus):
-        a, b = load(os.path.join(out, "run0"), r), load(os.path.join(out, "run1"), r)
-        first = None
-        for x, y in zip(a, b):
-            for key in ("loss", "pgrads", "grads", "grad_norm", "params"):
-                if x[key] != y[key]:
-                    diff = key
-                    if isinstance(x[key], list):
-                        idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
-                        diff = f"{key} (indices {idx[:8]}{'...' if len(idx) > 8 else ''} of {len(x[key])})"
-                    if key == "pgrads":
-                        names = a[0].get("names") or []
-                        diff += " " + str([names[j] for j in idx[:8]] if names else "")
-                    first = (x["step"], diff, x["loss"], y["loss"])
+    for k in range(1, runs):
+        for r in range(gpus):
+            a, b = load(os.path.join(out, "run0"), r), load(os.path.join(out, f"run{k}"), r)
+            first = None
+            for x, y in zip(a, b):
+                for key in ("loss", "pgrads", "grads", "grad_norm", "params"):
+                    if x[key] != y[key]:
+                        diff = key
+                        if isinstance(x[key], list):
+                            idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
+                            diff = f"{key} (indices {idx[:8]}{'...' if len(idx) > 8 else ''} of {len(x[key])})"
+                            if key in ("pgrads", "params"):
+                                names = a[0].get("names") or []
+                                diff += " " + str([names[j] for j in idx[:8]] if names else "")
+                        first = (x["step"], diff, x["loss"], y["loss"])
+                        break
+                if first:
                     break
-            if first:
-                break
-        print(f"rank {r}: " + ("identical" if first is None else
-                               f"first difference at step {first[0]}: {first[1]} (loss {first[2]} vs {first[3]})"),
-              flush=True)
+            print(f"run {k} vs run 0, rank {r}: " + ("identical" if first is None else
+                  f"first difference at step {first[0]}: {first[1]} (loss {first[2]} vs {first[3]})"), flush=True)
 
 
 if __name__ == "__main__":
