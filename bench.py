@@ -314,6 +314,17 @@ def _worker(a: argparse.Namespace) -> None:
 
     trace = os.environ.get("SCALING_AMD_BENCH_TRACE")  # race-check forensics: per-step values per rank (JSON lines)
     n_steps = [0]
+    pre: list = []
+    if trace:  # local gradients as the backward left them, before the optimizer step touches anything
+        orig_step = optimizer.step
+
+        def traced_step() -> Any:  # a stream-ordered snapshot (no host sync: it must not change the schedule)
+            with torch.no_grad():
+                pre[:] = [torch.stack([p.grad.double().sum() if p.grad is not None else p.new_zeros((), dtype=torch.float64)
+                                       for p in model.parameters()])]
+            return orig_step()
+
+        optimizer.step = traced_step
 
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,
@@ -328,7 +339,8 @@ def _worker(a: argparse.Namespace) -> None:
                        "grads": [float(g.grad_source().double().sum()) for g in optimizer.parameter_groups],
                        # local (pre-reduction) gradients: lazy zeroing leaves them in the flat buffer after the step
                        "pgrads": [float(p.grad.double().sum()) if p.grad is not None else None
-                                  for p in model.parameters()]}
+                                  for p in model.parameters()],
+                       "pgrads_pre": pre[0].tolist() if pre else []}
             with open(f"{trace}.rank{rank}.jsonl", "a") as f:
                 f.write(json.dumps(rec) + "\n")
         n_steps[0] += 1

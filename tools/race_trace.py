@@ -52,13 +52,13 @@ def main():
             a, b = load(os.path.join(out, "run0"), r), load(os.path.join(out, f"run{k}"), r)
             first = None
             for x, y in zip(a, b):
-                for key in ("loss", "pgrads", "grads", "grad_norm", "params"):
+                for key in ("loss", "pgrads_pre", "pgrads", "grads", "grad_norm", "params"):
                     if x[key] != y[key]:
                         diff = key
                         if isinstance(x[key], list):
                             idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
                             diff = f"{key} (indices {idx[:8]}{'...' if len(idx) > 8 else ''} of {len(x[key])})"
-                            if key in ("pgrads", "params"):
+                            if key in ("pgrads_pre", "pgrads", "params"):
                                 names = a[0].get("names") or []
                                 diff += " " + str([names[j] for j in idx[:8]] if names else "")
                         first = (x["step"], diff, x["loss"], y["loss"])
