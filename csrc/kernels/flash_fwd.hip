@@ -193,7 +193,7 @@ struct FwdV2 {
 // Variants measured against this one and dropped (8 waves per workgroup, inline-asm LDS-DMA, pinned read-ahead, an
 // 8-wave ping-pong schedule): profiles/attn_fwd_waves_ab_r2.log, attn_fwd_pingpong_ab_r3.log, attn_ab_r2_asyncdma.log;
 // their code is in git history before commit "Delete losing attention variants".
-template <int D, bool F16, bool DROP, bool RSM = true>
+template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     using C = FwdV2<D>;
@@ -263,13 +263,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) o[t] = f32x16{};
     float m = -INFINITY, l = 0.f;
-    // RSM: the row sum l as a fifth P.V product against an all-ones "V" (4 extra MFMAs per tile, MFMA pipe half idle)
-    // instead of 32 adds + a lane exchange on the issue-bound VALU; it sums the rounded P that P.V uses.  Not with
-    // dropout (the normaliser must see every p, P.V only the kept ones)
-    constexpr bool kRsm = RSM && !DROP;
-    f32x16 lacc = f32x16{};
-    const bf16x8 ones = __builtin_bit_cast(bf16x8, F16 ? u16x8{0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00}
-                                                       : u16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
     const float c2 = a.scale_log2;
     uint32_t drow = 0;
     if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
@@ -318,10 +311,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
             const float mnew = fmaxf(m, mrow);
             const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
             l *= alpha;
-            if constexpr (kRsm) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) lacc[j] *= alpha;
-            }
 #pragma unroll
             for (int t = 0; t < C::NT; ++t)
 #pragma unroll
@@ -329,23 +318,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
             m = mnew;
         }
         const float nm = m == -INFINITY ? 0.f : -m;
-        if constexpr (kRsm) {
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int j = 0; j < 16; ++j) s[b][j] = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
-        } else {
-            float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
-                    s[b][j] = p;
-                    rs[j & 3] += p;
-                }
-            l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
-        }
+            for (int j = 0; j < 16; ++j) {
+                const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
+                s[b][j] = p;
+                rs[j & 3] += p;
+            }
+        // (the row sum as a fifth P.V product against all-ones was measured slower: profiles/attn_rowsum_mfma_ab_r4.log)
+        l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
         if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
 #pragma unroll
             for (int b = 0; b < 2; ++b)
@@ -358,12 +341,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
-        if constexpr (kRsm) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) lacc = mma<F16>(ones, pf[b][ss], lacc);
-        }
         {
 #pragma unroll
             for (int t = 0; t < C::NT; ++t)
@@ -401,7 +378,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_FWD_ISSUE
-    if constexpr (kRsm) l = lacc[0];  // every row of the ones product holds the same sum
     if (myq < Lq) {
         const float inv = (l > 0.f ? 1.f / l : 0.f) * (DROP ? a.rp_drop : 1.f);
         u16* op = a.o + (int64_t)(q0s + myq) * a.o_tok + (int64_t)hq * a.o_head;
@@ -420,13 +396,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #endif
 }
 
-static int g_fa_rsm = 1;  // TEMPORARY A/B hook
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
         dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(256);
-        if (D == 128 && !g_fa_rsm) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, false>), grid, block, 4 * FwdV2<128>::TILE, st, a);
-        else if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
         else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
         return;
     }
@@ -435,7 +409,6 @@ static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
 }
 
 namespace sa_launch {
-void fa_set_rsm(int v) { g_fa_rsm = v; }
 void fa_fwd(const FwdArgs& a, int D, int max_q, bool f16, hipStream_t st) {
     const bool drop = a.p_drop > 0.f;
     if (f16) {

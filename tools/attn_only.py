@@ -40,23 +40,5 @@ def once():
     return f"fwd {fwd*1e3:.3f} ms {fl/fwd/1e12:.0f} TF | bwd {(tot-fwd)*1e3:.3f} ms {2.5*fl/(tot-fwd)/1e12:.0f} TF(2.5x)"
 
 
-from scaling_amd.ops._ext import ext  # noqa: E402
-
-if hasattr(ext(), "fa_set_rsm"):  # temporary A/B hook: row sum on MFMA (1) or VALU (0)
-    outs = {}
-    for var in (0, 1):
-        ext().fa_set_rsm(var)
-        qq, kk, vv = (t.detach().clone().requires_grad_(True) for t in (q, k, v))
-        oo = attention.flash_attention(qq, kk, vv, cu, cu, S, S, sc, True, None)
-        oo.backward(g)
-        outs[var] = (oo.detach().float(), qq.grad.float(), kk.grad.float(), vv.grad.float())
-    errs = [((x - y).abs().max() / y.abs().max()).item() for x, y in zip(outs[1], outs[0])]
-    print(f"rsm 1 vs 0: rel err o/dq/dk/dv {[round(e, 5) for e in errs]}", flush=True)
-    for _ in range(3):
-        for var in (0, 1):
-            ext().fa_set_rsm(var)
-            print(f"rsm {var}: {once()}", flush=True)
-    ext().fa_set_rsm(1)
-else:
-    for _ in range(3):
-        print(once(), flush=True)
+for _ in range(3):
+    print(once(), flush=True)

@@ -6,7 +6,7 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      1-GPU bench.py (BENCH_ARGS)
 #   prof       rocprofv3 --kernel-trace --stats of 3 bench steps + per-category summary of the last step
-#   pmc        SQ/MFMA counters of every kernel of a 4-layer 7B-width step (PMC_ARGS overrides the bench args)
+#   pmc        SQ/MFMA counters of every kernel of a 4-layer 7B-width step (PMC_PROG / PMC_ARGS: another program)
 #   gemm       tools/gemm_nt_bench.py (NT GEMM + SwiGLU epilogues vs hipBLASLt) and tools/gemm_nt_check.py
 #   attn       tools/attn_only.py (isolated attention at the 7B shape)
 #   decode     tools/decode_bench.py
@@ -35,7 +35,7 @@ for step in "$@"; do
             -- python3 "$R/bench.py" ${PROF_ARGS:---steps 3 --warmup 1} > "$R/gpurun_out/prof_$TAG.log" 2>&1)
         $PY tools/rocpd_step.py gpurun_out/prof_$TAG/run_results.db > gpurun_out/prof_step_$TAG.md 2>&1 || true ;;
     pmc)
-        B="$R/bench.py ${PMC_ARGS:---steps 1 --warmup 1 --num-layers 4}"
+        B="${PMC_PROG:-$R/bench.py} ${PMC_ARGS:---steps 1 --warmup 1 --num-layers 4}"
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
             SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
             GRBM_GUI_ACTIVE GRBM_COUNT -d "$R/gpurun_out/pmc_$TAG" -o a --output-format csv -- python3 $B \
