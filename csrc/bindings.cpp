@@ -749,7 +749,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
-    m.def("gemm_nt_set_variant", &sa_launch::gemm_nt_set_variant, "TEMPORARY A/B hook");
     m.def("gemm_nt_ok", &gemm_nt_ok, "whether gemm_nt supports these operands");
     m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16, 64-deep staged HIP kernel)");
     m.def("gemm_nt_swiglu_ok", &gemm_nt_swiglu_ok, "whether gemm_nt_swiglu supports these operands");

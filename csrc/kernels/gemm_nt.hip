@@ -54,7 +54,7 @@ __device__ __forceinline__ void hard_barrier() {
 }
 __device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
 
-template <int EPI, int VAR = 0>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
                                                          const u16* __restrict__ B, int ldb, uint32_t b_bytes, int M,
                                                          int N, int K, NtEpi ep) {
@@ -64,7 +64,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     const int wm = wave >> 1, wn = wave & 1;
     const int tm = M / 256, tn = N / 256;
     const int v = xcd_remap(blockIdx.x, tm * tn);
-    constexpr int GM = VAR == 2 ? 16 : VAR == 3 ? 4 : 8;  // TEMPORARY A/B: M-tile group height
+    // groups of GM M-tiles sweep N together; 4 beat 8 / 16 (profiles/gemm_nt_group_ab_r4.log)
+    constexpr int GM = 4;
     const int group = GM * tn;
     const int first_m = (v / group) * GM;
     const int gm = min(tm - first_m, GM);
@@ -269,8 +270,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                 u16x4 o;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e]);
-                if constexpr (VAR == 1) __builtin_nontemporal_store(o, reinterpret_cast<u16x4*>(cp + 16 * j));
-                else *reinterpret_cast<u16x4*>(cp + 16 * j) = o;
+                *reinterpret_cast<u16x4*>(cp + 16 * j) = o;
             }
         }
     } else if constexpr (EPI == EPI_SWIGLU) {
@@ -327,22 +327,14 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     }
 }
 #define SA_NT_INST(E)                                                                                          \
-    template __global__ void gemm_nt_kernel<E, 0>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int, \
+    template __global__ void gemm_nt_kernel<E>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int, \
                                                uint32_t, int, int, int, NtEpi);
 SA_NT_INST(EPI_STORE) SA_NT_INST(EPI_SWIGLU) SA_NT_INST(EPI_SWIGLU_BWD)
-template __global__ void gemm_nt_kernel<EPI_STORE, 1>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
-                                                      uint32_t, int, int, int, NtEpi);
-template __global__ void gemm_nt_kernel<EPI_STORE, 2>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
-                                                      uint32_t, int, int, int, NtEpi);
-template __global__ void gemm_nt_kernel<EPI_STORE, 3>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int,
-                                                      uint32_t, int, int, int, NtEpi);
 #undef SA_NT_INST
 
 }  // namespace sa_gemm_nt
 
 namespace sa_launch {
-static int g_nt_var = 0;  // TEMPORARY A/B hook
-void gemm_nt_set_variant(int v) { g_nt_var = v; }
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
     return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
            lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
@@ -358,9 +350,6 @@ void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, in
                        (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep)
     if (epi == EPI_SWIGLU) SA_NT_LAUNCH(EPI_SWIGLU);
     else if (epi == EPI_SWIGLU_BWD) SA_NT_LAUNCH(EPI_SWIGLU_BWD);
-    else if (g_nt_var == 1) hipLaunchKernelGGL((gemm_nt_kernel<EPI_STORE, 1>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep);
-    else if (g_nt_var == 2) hipLaunchKernelGGL((gemm_nt_kernel<EPI_STORE, 2>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep);
-    else if (g_nt_var == 3) hipLaunchKernelGGL((gemm_nt_kernel<EPI_STORE, 3>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab, (const u16*)B, (int)ldb, bb, (int)M, (int)N, (int)K, ep);
     else SA_NT_LAUNCH(EPI_STORE);
 #undef SA_NT_LAUNCH
 }

@@ -69,7 +69,6 @@ struct NtEpi {
     int F;                           // SwiGLU intermediate features
 };
 namespace sa_launch {
-void gemm_nt_set_variant(int v);
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                const NtEpi& ep, hipStream_t st);

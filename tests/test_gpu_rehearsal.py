@@ -115,7 +115,12 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
                          "runs repeat bit for bit (profiles/race_trace_r4.log, README 'Race check')"))),
         pytest.param(["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"},
                      marks=pytest.mark.xfail(strict=False, reason="as the DP2 delayed case")),
-        (["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {}),
+        pytest.param(["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {},
+                     marks=pytest.mark.xfail(strict=False, reason=(
+                         "open: with 8 ranks on the one GPU even the single-stream twin does not repeat bit for bit "
+                         "(pipeline stage-0 gradients of the first layer / embedding differ between single-stream "
+                         "runs, loss identical: profiles/race_trace_world8_r4.log), so the comparison has no fixed "
+                         "reference"))),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):

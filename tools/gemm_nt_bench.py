@@ -61,19 +61,7 @@ def main() -> None:
         if ext().gemm_nt_ok(x, w):
             ext().gemm_nt(x, w, c)
             r["err"] = ((c[:2048].float() - ref).abs().max() / ref.abs().max()).item()
-            if hasattr(ext(), "gemm_nt_set_variant"):  # temporary A/B hook
-                for var in range(4):
-                    ext().gemm_nt_set_variant(var)
-                    ext().gemm_nt(x, w, c)
-                    r[f"err{var}"] = ((c[:2048].float() - ref).abs().max() / ref.abs().max()).item()
-
-                    def arm(var=var):
-                        ext().gemm_nt_set_variant(var)
-                        ext().gemm_nt(x, w, c)
-                    arms[f"ours{var}"] = arm
-                ext().gemm_nt_set_variant(0)
-            else:
-                arms["ours"] = lambda: ext().gemm_nt(x, w, c)
+            arms["ours"] = lambda: ext().gemm_nt(x, w, c)
         ts = {k: [] for k in arms}
         for _ in range(a.rounds):
             for k, fn in arms.items():
