@@ -11,7 +11,8 @@
 // Numerics: every epilogue rounds the GEMM result to bf16 first and then applies exactly the arithmetic of the
 // stand-alone SwiGLU kernels (swiglu_rope.hip), so the fused and unfused paths agree.
 //
-// Structure (one 256x256 tile per workgroup, 4 waves = one per SIMD, each 128x128 of 16x16x32 MFMAs in AGPRs):
+// Structure (persistent: one workgroup per CU walks its 256x256 tiles; 4 waves = one per SIMD, each 128x128 of
+// 16x16x32 MFMAs in AGPRs):
 //  * 64-deep k-stages in five 32-KiB LDS images of [256 rows][64 k] bf16: A in two, B in three (see below);
 //  * LDS-DMA pieces (buffer_load ... lds) of 8 rows x 128 B: every lane group of 8 reads ONE full 128-B line
 //    (the previous 16-rows x 64-B pieces read half lines: twice the cache-line requests per byte);
@@ -22,8 +23,10 @@
 //    and issuing stage t+2's A pieces.  One barrier per 128 MFMAs, 8 DMA pieces per sub-step (a schedule with two
 //    stage buffers had to issue all 16 in one sub-step: 1.25-1.30 PF against 1.37-1.46 for this one,
 //    profiles/gemm_nt_split5_ab_r4.log).
-//  * grid: XCD-aware bijective remap, then 8-row groups of tiles (the 32 tiles resident on one XCD share A/B panels
-//    in its L2).
+//  * grid: XCD-aware bijective remap, then 4-row groups of tiles (the 32 tiles resident on one XCD share A/B panels
+//    in its L2);
+//  * the k-stage pipeline runs on across a workgroup's tiles: a tile's last two stages stage the next tile's first
+//    two, so neither the pipeline fill nor the epilogue's stores leave the MFMAs idle between tiles.
 // Reference op: F.linear at src/scaling/core/nn/linear/column_parallel_linear.py:151 / row_parallel_linear.py:158,
 // SwiGLU at src/scaling/core/nn/mlp.py:157-161.
 #include "common.h"
@@ -43,13 +46,16 @@ constexpr int kLds = 5 * kImg;      // A[0..1] + B[0..2]: all 160 KiB of LDS
 __device__ __forceinline__ void mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
+#ifndef NT_PROBE
+#define NT_PROBE 0  // TEMPORARY (tools/gemm_nt_probe.hip): 1 one k-slice, 2 no barriers, 3 no vm waits, 4 no DMA
+#endif
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    if (NT_PROBE != 3 && NT_PROBE != 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void hard_barrier() {
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
+    if (NT_PROBE != 2) asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
@@ -62,16 +68,23 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave >> 1, wn = wave & 1;
-    const int tm = M / 256, tn = N / 256;
-    const int v = xcd_remap(blockIdx.x, tm * tn);
-    // groups of GM M-tiles sweep N together; 4 beat 8 / 16 (profiles/gemm_nt_group_ab_r4.log)
-    constexpr int GM = 4;
-    const int group = GM * tn;
-    const int first_m = (v / group) * GM;
-    const int gm = min(tm - first_m, GM);
-    const int within = v % group;
-    const int m0 = (first_m + within % gm) * 256, nt = within / gm;
+    const int tm = M / 256, tn = N / 256, ntiles = tm * tn;
     const int T = K / 64;
+    // persistent: workgroup b takes virtual blocks b, b + G, ... (G = gridDim.x, a multiple of 8, so all on b's XCD);
+    // a virtual block maps to its tile as a one-tile-per-workgroup grid would: XCD-aware bijective remap, then groups
+    // of GM M-tiles sweeping N together (4 beat 8 / 16: profiles/gemm_nt_group_ab_r4.log)
+    constexpr int GM = 4;
+    auto tile_of = [&](int vb, int& tm0, int& tnt) {
+        const int v = xcd_remap(vb, ntiles);
+        const int group = GM * tn;
+        const int first_m = (v / group) * GM;
+        const int gm = min(tm - first_m, GM);
+        const int within = v % group;
+        tm0 = (first_m + within % gm) * 256;
+        tnt = within / gm;
+    };
+    int tile = blockIdx.x, m0, nt;
+    tile_of(tile, m0, nt);
 
     // ---- LDS-DMA: wave w stages pieces P = w + 4i (image rows 8P .. 8P+7) of each operand; lane -> (row lane >> 3,
     // 16-B slot lane & 7), source chunk = slot ^ f(row), f = (row >> 1) & 7 = 4 (P & 1) + (lane >> 4) (piece-invariant)
@@ -79,20 +92,17 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     const int pch = (lane & 7) ^ ((((wave & 1) << 2) | (lane >> 4)) & 7);
     const int va = (prow * lda + 8 * pch) * 2;
     const int vb = (prow * ldb + 8 * pch) * 2;
-    const int abase = __builtin_amdgcn_readfirstlane((m0 + 8 * wave) * lda * 2);
+    auto a_base = [&](int tm0) { return __builtin_amdgcn_readfirstlane((tm0 + 8 * wave) * lda * 2); };
+    auto b_base = [&](int tnt) {
+        // SWIGLU: image rows 16 jb .. +15: jb even = gate rows, jb odd = up rows of features f0 + 16 (jb >> 1) ..;
+        // piece P = w + 4i has jb = P >> 1: gate/up by (w >> 1) & 1, feature block i, half (w & 1)
+        const int brow0 =
+            EPI == EPI_SWIGLU ? ((wave >> 1) & 1) * ep.F + tnt * 128 + (wave & 1) * 8 : tnt * 256 + 8 * wave;
+        return __builtin_amdgcn_readfirstlane(brow0 * ldb * 2);
+    };
+    int abase = a_base(m0), bbase = b_base(nt);
     const int astep = __builtin_amdgcn_readfirstlane(32 * lda * 2);
-    int brow0, bsteprows;
-    if constexpr (EPI == EPI_SWIGLU) {
-        // image rows 16 jb .. +15: jb even = gate rows, jb odd = up rows of features f0 + 16 (jb >> 1) ..; piece P = w + 4i
-        // has jb = P >> 1: gate/up by (w >> 1) & 1, feature block i, half (w & 1)
-        brow0 = ((wave >> 1) & 1) * ep.F + nt * 128 + (wave & 1) * 8;
-        bsteprows = 16;
-    } else {
-        brow0 = nt * 256 + 8 * wave;
-        bsteprows = 32;
-    }
-    const int bbase = __builtin_amdgcn_readfirstlane(brow0 * ldb * 2);
-    const int bstep = __builtin_amdgcn_readfirstlane(bsteprows * ldb * 2);
+    const int bstep = __builtin_amdgcn_readfirstlane((EPI == EPI_SWIGLU ? 16 : 32) * ldb * 2);
     typedef int i32x4 __attribute__((ext_vector_type(4)));
     const i32x4 rsa = {(int)__builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uint64_t>(A)),
                        (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(A) >> 32)) & 0xffff),
@@ -101,38 +111,37 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                        (int)(__builtin_amdgcn_readfirstlane((uint32_t)(reinterpret_cast<uint64_t>(B) >> 32)) & 0xffff),
                        (int)__builtin_amdgcn_readfirstlane(b_bytes), fa::kBufFlags};
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((lds_void*)smem));
-    // piece P (0..15; even: A piece P/2, odd: B piece P/2) of stage U into stage buffer BUF.  Inline asm so the
-    // waitcnt pass does not drain the pipeline in front of every ds_read (it cannot tell which LDS bytes a
-    // compiler-visible LDS-DMA writes); m0 is written in the statement that reads it.
-#define NT_PIECE_AT(ISB, I, LBASE, U)                                                                             \
+    // piece I of operand A / B (ISB) of k-stage KU of the tile whose operand base is BASE, into the image at LBASE.
+    // Inline asm so the waitcnt pass does not drain the pipeline in front of every ds_read (it cannot tell which LDS
+    // bytes a compiler-visible LDS-DMA writes); m0 is written in the statement that reads it.
+#define NT_PIECE_AT(ISB, I, LBASE, KU, BASE)                                                                      \
     {                                                                                                             \
         const uint32_t l_ = (LBASE) + (wave + 4 * (I)) * 1024;                                                    \
-        const int ku_ = (U) * 128;                                                                                \
         if (ISB)                                                                                                  \
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
-                         "v"(vb), "s"(rsb), "s"(bbase + (I) * bstep + ku_)                                         \
+                         "v"(vb), "s"(rsb), "s"((BASE) + (I) * bstep + (KU) * 128)                                 \
                          : "m0");                                                                                 \
         else                                                                                                      \
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(l_),     \
-                         "v"(va), "s"(rsa), "s"(abase + (I) * astep + ku_)                                         \
+                         "v"(va), "s"(rsa), "s"((BASE) + (I) * astep + (KU) * 128)                                 \
                          : "m0");                                                                                 \
     }
     // in the loop: the piece together with the MFMA before it, in one statement -- the MFMA is the wait state between
-    // the M0 write and the LDS-DMA instead of an s_nop issue slot (+1.6-3 %, profiles/gemm_nt_mfma_piece_ab_r4.log)
-#define NT_MFMA_PIECE_AT(C_, A_, B_, ISB, I, LBASE, U)                                                              \
+    // the M0 write and the LDS-DMA instead of an s_nop issue slot (+1.6-3 %, profiles/gemm_nt_mfma_piece_ab_r4.log).
+    // ZC "%0" accumulates, "0" starts the accumulator (first k-slice of a tile)
+#define NT_MFMA_PIECE_AT(C_, A_, B_, ISB, I, LBASE, KU, BASE, ZC)                                                   \
     {                                                                                                             \
         const uint32_t l_ = (LBASE) + (wave + 4 * (I)) * 1024;                                                    \
-        const int ku_ = (U) * 128;                                                                                \
         if (ISB)                                                                                                  \
-            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                      \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, " ZC "\n\t"                  \
                          "buffer_load_dwordx4 %4, %5, %6 offen lds"                                               \
                          : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(vb), "s"(rsb),                               \
-                           "s"(bbase + (I) * bstep + ku_) : "m0");                                                 \
+                           "s"((BASE) + (I) * bstep + (KU) * 128) : "m0");                                         \
         else                                                                                                      \
-            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0\n\t"                      \
+            asm volatile("s_mov_b32 m0, %3\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, " ZC "\n\t"                  \
                          "buffer_load_dwordx4 %4, %5, %6 offen lds"                                               \
                          : "+a"(C_) : "v"(A_), "v"(B_), "s"(l_), "v"(va), "s"(rsa),                               \
-                           "s"(abase + (I) * astep + ku_) : "m0");                                                 \
+                           "s"((BASE) + (I) * astep + (KU) * 128) : "m0");                                         \
     }
 
     f32x4 acc[8][8];
@@ -153,7 +162,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     // barrier t), so every sub-step carries 8 DMA pieces + 16 fragment reads beside its 64 MFMAs instead of one
     // sub-step carrying all 16 pieces.  End of (t, 0): own reads retired, vmcnt(8) (stage t+1 landed, the 8 B pieces
     // of stage t+2 just issued stay in flight), barrier t.  The B buffer roles rotate in registers (cur, next,
-    // next-next), the A buffers by the 2-stage unroll.
+    // next-next), the A buffers by the 2-stage unroll.  Stages count on across the tiles of a workgroup: the last two
+    // stages of a tile stage the next tile's first two (the pipeline never drains between tiles, and the epilogue's
+    // stores overlap those loads); after the last tile they re-stage the tile's own first two (never read).
     int oa[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -175,14 +186,16 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         lbc = lbn; lbn = lbnn; lbnn = tl_;                                                                        \
         asm volatile("" : "+v"(obc0), "+v"(obc1), "+v"(obn0), "+v"(obn1), "+v"(obnn0), "+v"(obnn1));             \
     }
-    // sub-step (U, 0), A buffer SA: MFMAs on F0, F1 read one fragment per 3 MFMAs over the first 48, stage U+2's
-    // B pieces (PIECES) one per 8 MFMAs; retire own reads + stage U+1, barrier
-#define NT5_SUB0(SA, U, PIECES)                                                                                   \
+    // sub-step (t, 0), A buffer SA: MFMAs on F0, F1 read one fragment per 3 MFMAs over the first 48, the B pieces of
+    // k-stage KU (= t + 2, or 0 / 1 of the next tile) from operand base BB one per 8 MFMAs; retire own reads + stage
+    // t+1, barrier.  ZC "0": first k-slice of the tile (starts the accumulators)
+#define NT5_SUB0(SA, KU, BB, ZC)                                                                                  \
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
             const int m_ = i * 8 + j;                                                                             \
-            if ((PIECES) && (m_ & 7) == 7) NT_MFMA_PIECE_AT(acc[i][j], fb0[j], fa0[i], true, m_ >> 3, lbnn, (U) + 2) \
-            else mfma(acc[i][j], fb0[j], fa0[i]);                                                                 \
+            if (NT_PROBE != 4 && (m_ & 7) == 7)                                                                   \
+                NT_MFMA_PIECE_AT(acc[i][j], fb0[j], fa0[i], true, m_ >> 3, lbnn, KU, BB, ZC)                      \
+            else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, " ZC : "+a"(acc[i][j]) : "v"(fb0[j]), "v"(fa0[i]));\
             if (m_ % 3 == 1 && m_ < 48) {                                                                         \
                 const int f_ = m_ / 3;                                                                            \
                 if (f_ < 8) fb1[f_] = frag(obc1, f_);                                                             \
@@ -190,21 +203,20 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
             }                                                                                                     \
         }                                                                                                         \
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                        \
-        if (PIECES) wait_vm<8>();                                                                                 \
-        else wait_vm<0>();                                                                                        \
+        wait_vm<8>();                                                                                             \
         hard_barrier();                                                                                           \
     }
-    // sub-step (U, 1): MFMAs on F1, F0 of stage U+1 (NEXT) read one per 3 MFMAs over the first 48, stage U+2's A
-    // pieces into A[SA] (PIECES) one per 8 MFMAs (one per 4 over the first 32: 0-1.6 % slower,
+    // sub-step (t, 1): MFMAs on F1, F0 of stage t+1 read one per 3 MFMAs over the first 48, the A pieces of k-stage
+    // KU from operand base AB into A[SA] one per 8 MFMAs (one per 4 over the first 32: 0-1.6 % slower,
     // profiles/gemm_nt_apiece_ab_r4.log)
-#define NT5_SUB1(SA, U, NEXT, PIECES)                                                                             \
+#define NT5_SUB1(SA, KU, AB)                                                                                      \
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
             const int m_ = i * 8 + j;                                                                             \
-            if ((PIECES) && (m_ & 7) == 3)                                                                        \
-                NT_MFMA_PIECE_AT(acc[i][j], fb1[j], fa1[i], false, m_ >> 3, lds0 + (SA) * kImg, (U) + 2)          \
+            if (NT_PROBE != 4 && (m_ & 7) == 3)                                                                   \
+                NT_MFMA_PIECE_AT(acc[i][j], fb1[j], fa1[i], false, m_ >> 3, lds0 + (SA) * kImg, KU, AB, "%0")     \
             else mfma(acc[i][j], fb1[j], fa1[i]);                                                                 \
-            if ((NEXT) && m_ % 3 == 1 && m_ < 48) {                                                               \
+            if (m_ % 3 == 1 && m_ < 48) {                                                                         \
                 const int f_ = m_ / 3;                                                                            \
                 if (f_ < 8) fb0[f_] = frag(obn0, f_);                                                             \
                 else fa0[f_ - 8] = frag(oa[(SA) ^ 1][0], f_ - 8);                                                 \
@@ -212,19 +224,19 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         }                                                                                                         \
         NT5_ROTATE()                                                                                              \
     }
-    // prologue: stages 0 and 1 in flight (A[0] B[0], A[1] B[1]), stage 0 landed, barrier, F0 of stage 0
+    // prologue: stages 0 and 1 of the first tile in flight (A[0] B[0], A[1] B[1]), stage 0 landed, barrier, F0
     // the DMA descriptors / offsets may be fresh from v_readfirstlane (a VALU write of an SGPR that an inline-asm
     // buffer_load reads needs 5 wait states the compiler cannot see)
     asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        NT_PIECE_AT(false, i, lds0, 0)
-        NT_PIECE_AT(true, i, lds0 + 2 * kImg, 0)
+        NT_PIECE_AT(false, i, lds0, 0, abase)
+        NT_PIECE_AT(true, i, lds0 + 2 * kImg, 0, bbase)
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        NT_PIECE_AT(false, i, lds0 + kImg, 1)
-        NT_PIECE_AT(true, i, lds0 + 3 * kImg, 1)
+        NT_PIECE_AT(false, i, lds0 + kImg, 1, abase)
+        NT_PIECE_AT(true, i, lds0 + 3 * kImg, 1, bbase)
     }
     wait_vm<16>();
     hard_barrier();
@@ -233,98 +245,116 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
         if (f < 8) fb0[f] = frag(obc0, f);
         else fa0[f - 8] = frag(oa[0][0], f - 8);
     }
-    int u = 0;
-    for (; u < T - 2; u += 2) {  // T even (K % 128 == 0, checked by the dispatcher)
-        NT5_SUB0(0, u, true)
-        NT5_SUB1(0, u, true, true)
-        NT5_SUB0(1, u + 1, true)
-        NT5_SUB1(1, u + 1, true, true)
-    }
-    NT5_SUB0(0, u, false)
-    NT5_SUB1(0, u, true, false)
-    NT5_SUB0(1, u + 1, false)
-    NT5_SUB1(1, u + 1, false, false)
-#undef NT5_SUB0
-#undef NT5_SUB1
-#undef NT5_ROTATE
-#undef NT_PIECE_AT
-#undef NT_MFMA_PIECE_AT
-    wait_vm<0>();
-    // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the accumulators,
-    // and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without it hipcc hoists
-    // the first v_accvgpr_reads in among the last MFMAs, which then read stale AGPRs)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    for (;;) {
+        const int next = tile + (int)gridDim.x;
+        const bool more = next < ntiles;  // workgroup-uniform
+        int nm0, nnt;
+        tile_of(more ? next : tile, nm0, nnt);
+        const int nab = a_base(nm0), nbb = b_base(nnt);
+        asm volatile("s_nop 4" ::: "memory");
+        NT5_SUB0(0, 2, bbase, "0")
+        NT5_SUB1(0, 2, abase)
+        NT5_SUB0(1, 3, bbase, "%0")
+        NT5_SUB1(1, 3, abase)
+        for (int u = 2; u < T - 2; u += 2) {  // T even and >= 4 (checked by the dispatcher)
+            NT5_SUB0(0, u + 2, bbase, "%0")
+            NT5_SUB1(0, u + 2, abase)
+            NT5_SUB0(1, u + 3, bbase, "%0")
+            NT5_SUB1(1, u + 3, abase)
+        }
+        NT5_SUB0(0, 0, nbb, "%0")
+        NT5_SUB1(0, 0, nab)
+        NT5_SUB0(1, 1, nbb, "%0")
+        NT5_SUB1(1, 1, nab)
+        // the MFMAs are inline asm, invisible to the hazard recognizer: cover the MFMA -> VALU read of the
+        // accumulators, and pin every accumulator read behind that cover (an empty "+a" asm per accumulator: without
+        // it hipcc hoists the first v_accvgpr_reads in among the last MFMAs, which then read stale AGPRs)
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
-    // ---- epilogue: acc[i][j][e] = C[m0 + 128 wm + 16 i + (lane & 15)][tile col 128 wn + 16 j + 4 (lane >> 4) + e]
-    const int r = lane & 15, q4 = 4 * (lane >> 4);
-    if constexpr (EPI == EPI_STORE) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            u16* cp = ep.C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ep.ldc + nt * 256 + 128 * wn + q4;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                u16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e]);
-                *reinterpret_cast<u16x4*>(cp + 16 * j) = o;
+        // ---- epilogue: acc[i][j][e] = C[m0 + 128 wm + 16 i + (lane & 15)][tile col 128 wn + 16 j + 4 (lane >> 4) + e]
+        const int r = lane & 15, q4 = 4 * (lane >> 4);
+        if constexpr (EPI == EPI_STORE) {
+    #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                u16* cp = ep.C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ep.ldc + nt * 256 + 128 * wn + q4;
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    u16x4 o;
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[i][j][e]);
+                    *reinterpret_cast<u16x4*>(cp + 16 * j) = o;
+                }
+            }
+        } else if constexpr (EPI == EPI_SWIGLU) {
+            // j = 2 jj: gate, j = 2 jj + 1: up of features nt * 128 + 64 wn + 16 jj + q4 + e
+    #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int64_t row = m0 + 128 * wm + 16 * i + r;
+                const int f = nt * 128 + 64 * wn + q4;
+    #pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    u16x4 gz, uz, hz;
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        gz[e] = f2bf(acc[i][2 * jj][e]);
+                        uz[e] = f2bf(acc[i][2 * jj + 1][e]);
+                        hz[e] = f2bf(round_bf(silu_f(bf2f(gz[e]))) * bf2f(uz[e]));
+                    }
+                    if (ep.C) {
+                        *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + f + 16 * jj) = gz;
+                        *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + ep.F + f + 16 * jj) = uz;
+                    }
+                    *reinterpret_cast<u16x4*>(ep.H + row * ep.ldh + f + 16 * jj) = hz;
+                }
+            }
+        } else {  // EPI_SWIGLU_BWD: tile column = feature
+    #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int64_t row = m0 + 128 * wm + 16 * i + r;
+                const u16* zp = ep.Z + row * ep.ldz + nt * 256 + 128 * wn + q4;
+                u16* dp = ep.C + row * ep.ldc + nt * 256 + 128 * wn + q4;
+                u16x4 gz[8], uz[8];
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    gz[j] = *reinterpret_cast<const u16x4*>(zp + 16 * j);
+                    uz[j] = *reinterpret_cast<const u16x4*>(zp + ep.F + 16 * j);
+                }
+    #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    u16x4 da, db;
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float g = round_bf(acc[i][j][e]);
+                        const float av = bf2f(gz[j][e]), bv = bf2f(uz[j][e]);
+                        const float sig = 1.f / (1.f + __expf(-av));
+                        const float s = av * sig;
+                        db[e] = f2bf(g * round_bf(s));
+                        const float ds = g * bv;
+                        da[e] = f2bf(ds * (sig * (1.f + av * (1.f - sig))));
+                    }
+                    *reinterpret_cast<u16x4*>(dp + 16 * j) = da;
+                    *reinterpret_cast<u16x4*>(dp + ep.F + 16 * j) = db;
+                }
             }
         }
-    } else if constexpr (EPI == EPI_SWIGLU) {
-        // j = 2 jj: gate, j = 2 jj + 1: up of features nt * 128 + 64 wn + 16 jj + q4 + e
+        // the next tile's first MFMAs overwrite the accumulators the epilogue just read
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int64_t row = m0 + 128 * wm + 16 * i + r;
-            const int f = nt * 128 + 64 * wn + q4;
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                u16x4 gz, uz, hz;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    gz[e] = f2bf(acc[i][2 * jj][e]);
-                    uz[e] = f2bf(acc[i][2 * jj + 1][e]);
-                    hz[e] = f2bf(round_bf(silu_f(bf2f(gz[e]))) * bf2f(uz[e]));
-                }
-                if (ep.C) {
-                    *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + f + 16 * jj) = gz;
-                    *reinterpret_cast<u16x4*>(ep.C + row * ep.ldc + ep.F + f + 16 * jj) = uz;
-                }
-                *reinterpret_cast<u16x4*>(ep.H + row * ep.ldh + f + 16 * jj) = hz;
-            }
-        }
-    } else {  // EPI_SWIGLU_BWD: tile column = feature
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int64_t row = m0 + 128 * wm + 16 * i + r;
-            const u16* zp = ep.Z + row * ep.ldz + nt * 256 + 128 * wn + q4;
-            u16* dp = ep.C + row * ep.ldc + nt * 256 + 128 * wn + q4;
-            u16x4 gz[8], uz[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                gz[j] = *reinterpret_cast<const u16x4*>(zp + 16 * j);
-                uz[j] = *reinterpret_cast<const u16x4*>(zp + ep.F + 16 * j);
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                u16x4 da, db;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float g = round_bf(acc[i][j][e]);
-                    const float av = bf2f(gz[j][e]), bv = bf2f(uz[j][e]);
-                    const float sig = 1.f / (1.f + __expf(-av));
-                    const float s = av * sig;
-                    db[e] = f2bf(g * round_bf(s));
-                    const float ds = g * bv;
-                    da[e] = f2bf(ds * (sig * (1.f + av * (1.f - sig))));
-                }
-                *reinterpret_cast<u16x4*>(dp + 16 * j) = da;
-                *reinterpret_cast<u16x4*>(dp + ep.F + 16 * j) = db;
-            }
-        }
+            for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+        asm volatile("s_nop 4" ::: "memory");
+        if (!more) break;
+        tile = next;
+        m0 = nm0;
+        nt = nnt;
+        abase = nab;
+        bbase = nbb;
     }
+    wait_vm<0>();  // the re-staged pieces of the last tile land before the workgroup's LDS is released
 }
 #define SA_NT_INST(E)                                                                                          \
     template __global__ void gemm_nt_kernel<E>(const u16* __restrict__, int, uint32_t, const u16* __restrict__, int, \
@@ -336,14 +366,22 @@ SA_NT_INST(EPI_STORE) SA_NT_INST(EPI_SWIGLU) SA_NT_INST(EPI_SWIGLU_BWD)
 
 namespace sa_launch {
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
-    return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-           lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&
-           (M / 256) * (N / 256) < (int64_t(1) << 31);
+    return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && K >= 256 && M > 0 && N > 0 && lda % 8 == 0 &&
+           ldb % 8 == 0 && lda >= K && ldb >= K && M * lda * 2 < (int64_t(1) << 31) &&
+           N * ldb * 2 < (int64_t(1) << 31) && (M / 256) * (N / 256) < (int64_t(1) << 31);
 }
 void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                const NtEpi& ep, hipStream_t st) {
     using namespace sa_gemm_nt;
-    const int nwg = (int)((M / 256) * (N / 256));
+    static const int ncu = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
+            n = 256;
+        return n - n % 8;
+    }();
+    const int ntiles = (int)((M / 256) * (N / 256));
+    const int nwg = ntiles < ncu ? ntiles : ncu;  // persistent: one workgroup per CU (160 KiB of LDS each)
     const uint32_t ab = (uint32_t)(M * lda * 2), bb = (uint32_t)(N * ldb * 2);
 #define SA_NT_LAUNCH(E)                                                                                         \
     hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(nwg), dim3(256), kLds, st, (const u16*)A, (int)lda, ab,         \

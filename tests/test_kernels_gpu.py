@@ -528,10 +528,12 @@ def test_gemm_tn(M, N, K, accumulate):
     assert not ext().gemm_tn_ok(A[:64], B[:64], C)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2),
+                                   (8192, 2304, 256), (4352, 4096, 384)])
 def test_gemm_nt(M, N, K):
     """Forward / dgrad GEMM C = A B^T (64-deep staged kernel, csrc/kernels/gemm_nt.hip) against an fp32 reference,
-    with a strided (sliced) A and an asymmetric B."""
+    with a strided (sliced) A and an asymmetric B.  The last two shapes have more tiles than CUs (288, 272), so
+    workgroups of the persistent kernel walk several tiles with the pipeline running on across them."""
     torch.manual_seed(7)
     A_full = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
     A = A_full[:, 64:]
@@ -543,9 +545,10 @@ def test_gemm_nt(M, N, K):
     torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
     assert not ext().gemm_nt_ok(A[:200], B)
     assert not ext().gemm_nt_ok(A[:, : K - 64], B[:, : K - 64])
+    assert not ext().gemm_nt_ok(A[:, :128], B[:, :128])  # fewer than 4 k-stages
 
 
-@pytest.mark.parametrize("M,F,K", [(256, 256, 128), (512, 512, 256), (1024, 1024, 512)])
+@pytest.mark.parametrize("M,F,K", [(256, 256, 256), (512, 512, 256), (1024, 1024, 512), (8192, 2304, 256)])
 def test_gemm_nt_swiglu_epilogues(M, F, K):
     """Fused SwiGLU epilogues of the NT GEMM: forward (z = x [W_g; W_u]^T, h = silu(g) u) and backward
     (dz = swiglu_bwd(dY W_down, z)) are bit-identical to the unfused GEMM + SwiGLU kernels, and match an fp32
