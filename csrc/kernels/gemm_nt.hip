@@ -46,16 +46,13 @@ constexpr int kLds = 5 * kImg;      // A[0..1] + B[0..2]: all 160 KiB of LDS
 __device__ __forceinline__ void mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
-#ifndef NT_PROBE
-#define NT_PROBE 0  // TEMPORARY (tools/gemm_nt_probe.hip): 1 one k-slice, 2 no barriers, 3 no vm waits, 4 no DMA
-#endif
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    if (NT_PROBE != 3 && NT_PROBE != 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void hard_barrier() {
     __builtin_amdgcn_sched_barrier(0);
-    if (NT_PROBE != 2) asm volatile("s_barrier" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ float silu_f(float a) { return a / (1.f + __expf(-a)); }
@@ -193,7 +190,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
             const int m_ = i * 8 + j;                                                                             \
-            if (NT_PROBE != 4 && (m_ & 7) == 7)                                                                   \
+            if ((m_ & 7) == 7)                                                                   \
                 NT_MFMA_PIECE_AT(acc[i][j], fb0[j], fa0[i], true, m_ >> 3, lbnn, KU, BB, ZC)                      \
             else asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, " ZC : "+a"(acc[i][j]) : "v"(fb0[j]), "v"(fa0[i]));\
             if (m_ % 3 == 1 && m_ < 48) {                                                                         \
@@ -213,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     {                                                                                                             \
         _Pragma("unroll") for (int i = 0; i < 8; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) {             \
             const int m_ = i * 8 + j;                                                                             \
-            if (NT_PROBE != 4 && (m_ & 7) == 3)                                                                   \
+            if ((m_ & 7) == 3)                                                                   \
                 NT_MFMA_PIECE_AT(acc[i][j], fb1[j], fa1[i], false, m_ >> 3, lds0 + (SA) * kImg, KU, AB, "%0")     \
             else mfma(acc[i][j], fb1[j], fa1[i]);                                                                 \
             if (m_ % 3 == 1 && m_ < 48) {                                                                         \

@@ -21,8 +21,9 @@ def err(M, N, K, x=None, w=None):
     return (d.max() / ref.abs().max()).item(), bad.mean().item(), bad
 
 
-for (M, N, K) in [(256, 256, 128), (256, 256, 256), (256, 256, 1024), (256, 256, 4096), (512, 512, 4096),
-                  (2048, 2048, 4096), (4096, 4096, 4096)]:
+# the last three have more tiles than CUs: persistent workgroups walk 1-3 tiles each
+for (M, N, K) in [(256, 256, 256), (256, 256, 1024), (256, 256, 4096), (512, 512, 4096), (2048, 2048, 4096),
+                  (4096, 4096, 4096), (8192, 2304, 256), (4352, 4096, 384), (4096, 8448, 512)]:
     e, frac, bad = err(M, N, K)
     msg = f"M{M} N{N} K{K}: max_rel_err {e:.4f} bad_frac {frac:.4f}"
     if frac > 0:

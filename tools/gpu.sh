@@ -8,7 +8,6 @@
 #   prof       rocprofv3 --kernel-trace --stats of 3 bench steps + per-category summary of the last step
 #   pmc        SQ/MFMA counters of every kernel of a 4-layer 7B-width step (PMC_PROG / PMC_ARGS: another program)
 #   gemm       tools/gemm_nt_bench.py (NT GEMM + SwiGLU epilogues vs hipBLASLt) and tools/gemm_nt_check.py
-#   probe      tools/bin/gemm_nt_probe_* (built from tools/gemm_nt_probe.hip with -DNT_PROBE=...)
 #   attn       tools/attn_only.py (isolated attention at the 7B shape)
 #   decode     tools/decode_bench.py
 #   race       the multi- vs single-stream race check (tests/test_gpu_rehearsal.py -k race_check)
@@ -45,8 +44,6 @@ for step in "$@"; do
     gemm)
         $T 300 $PY tools/gemm_nt_check.py > gpurun_out/gemm_check_$TAG.log 2>&1
         $T 400 $PY tools/gemm_nt_bench.py ${GEMM_ARGS:---rounds 3 --iters 8} > gpurun_out/gemm_$TAG.log 2>&1 ;;
-    probe)
-        for b in tools/bin/gemm_nt_probe_*; do $T 120 ./$b >> gpurun_out/probe_$TAG.log 2>&1; done ;;
     attn)
         $T 300 $PY tools/attn_only.py ${ATTN_ARGS:-} > gpurun_out/attn_$TAG.log 2>&1 ;;
     decode)
