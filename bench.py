@@ -29,7 +29,6 @@ import argparse
 import json
 import os
 import signal
-import socket
 import subprocess
 import sys
 import time
@@ -125,9 +124,9 @@ def _env_int(k: str, d: int) -> int:
 
 # ---------------------------------------------------------------------------------------------- launcher
 def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return int(s.getsockname()[1])
+    from scaling_amd.core.utils.port import find_free_port  # outside the ephemeral range (no EADDRINUSE race)
+
+    return find_free_port()
 
 
 def _launch(a: argparse.Namespace) -> int:

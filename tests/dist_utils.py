@@ -2,7 +2,6 @@
 from __future__ import annotations
 
 import os
-import socket
 import traceback
 from typing import Any, Callable
 
@@ -10,9 +9,9 @@ import torch.multiprocessing as mp
 
 
 def free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from scaling_amd.core.utils.port import find_free_port
+
+    return find_free_port()
 
 
 def _entry(rank: int, world_size: int, port: int, fn: Callable, kwargs: dict, q: Any) -> None:
