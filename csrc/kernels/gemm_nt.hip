@@ -309,24 +309,31 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
                 }
             }
         } else {  // EPI_SWIGLU_BWD: tile column = feature
-    #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int64_t row = m0 + 128 * wm + 16 * i + r;
-                const u16* zp = ep.Z + row * ep.ldz + nt * 256 + 128 * wn + q4;
-                u16* dp = ep.C + row * ep.ldc + nt * 256 + 128 * wn + q4;
-                u16x4 gz[8], uz[8];
-    #pragma unroll
+            // z of row block i + 1 is loaded before row block i is computed and stored: every wait is for loads
+            // issued one block earlier, not for a full memory round trip per block
+            const u16* zrow = ep.Z + (int64_t)(m0 + 128 * wm + r) * ep.ldz + nt * 256 + 128 * wn + q4;
+            u16x4 gz[2][8], uz[2][8];
+            auto zload = [&](int bb, int i) {
+                const u16* zp = zrow + (int64_t)(16 * i) * ep.ldz;
+#pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    gz[j] = *reinterpret_cast<const u16x4*>(zp + 16 * j);
-                    uz[j] = *reinterpret_cast<const u16x4*>(zp + ep.F + 16 * j);
+                    gz[bb][j] = *reinterpret_cast<const u16x4*>(zp + 16 * j);
+                    uz[bb][j] = *reinterpret_cast<const u16x4*>(zp + ep.F + 16 * j);
                 }
-    #pragma unroll
+            };
+            zload(0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 1 < 8) zload((i + 1) & 1, i + 1);
+                const int64_t row = m0 + 128 * wm + 16 * i + r;
+                u16* dp = ep.C + row * ep.ldc + nt * 256 + 128 * wn + q4;
+#pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     u16x4 da, db;
-    #pragma unroll
+#pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float g = round_bf(acc[i][j][e]);
-                        const float av = bf2f(gz[j][e]), bv = bf2f(uz[j][e]);
+                        const float av = bf2f(gz[i & 1][j][e]), bv = bf2f(uz[i & 1][j][e]);
                         const float sig = 1.f / (1.f + __expf(-av));
                         const float s = av * sig;
                         db[e] = f2bf(g * round_bf(s));
