@@ -4,7 +4,7 @@
 but runs ``dense_in``/``siglu_weight`` as one fused GEMM whose ``[..., 2F]`` output feeds the HIP
 SwiGLU kernel directly (and whose backward receives the fused gradient from that kernel).
 
-With the HIP NT GEMM enabled for its shapes (``ops.gemm.nt_enabled``; model-parallel size 1, no biases, outside a
+With the fused node enabled for its shapes (``ops.gemm.nt_fused_mlp_enabled``; model-parallel size 1, no biases, outside a
 GEMM-keeping activation-checkpoint region) the whole MLP is ONE autograd node on the NT kernel's fused epilogues
 (``_SwiGLUMLPFused``): the gate/up GEMM writes ``z = [g | u]`` and ``h = silu(g) u`` in one pass, and the backward's
 down-projection input gradient consumes ``dh`` in registers and writes ``dz`` directly -- no SwiGLU pass over HBM in
@@ -19,7 +19,7 @@ import torch
 from ...ops import swiglu as swiglu_ops
 from ...ops._ext import ext, use_native
 from ...ops.attention import stash_active
-from ...ops.gemm import mm_nt, nt_enabled, transpose2d
+from ...ops.gemm import mm_nt, nt_fused_mlp_enabled, transpose2d
 from ..topology import Topology
 from .activation_function import ActivationFunction, get_activation_function
 from .linear import ColumnParallelLinear, RowParallelLinear
@@ -199,7 +199,7 @@ class ParallelSwiGLUMLP(torch.nn.Module):
             return False
         wgu = adjacent_weights([self.dense_in.weight, self.siglu_weight.weight])
         x2 = x.reshape(-1, x.shape[-1])
-        return (wgu is not None and nt_enabled(x2, wgu) and bool(ext().gemm_nt_swiglu_ok(x2, wgu))
+        return (wgu is not None and nt_fused_mlp_enabled(x2, wgu) and bool(ext().gemm_nt_swiglu_ok(x2, wgu))
                 and self.dense_out.weight.shape[1] % 256 == 0 and x.shape[-1] % 256 == 0)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

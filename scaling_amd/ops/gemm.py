@@ -53,6 +53,23 @@ _NT_MODE = os.environ.get("SCALING_AMD_NT_GEMM", "auto")
 NT_FASTER: set[tuple[int, int]] = set()
 
 
+# (2F, H) gate/up weight shapes where the one-node SwiGLU MLP on the NT kernel's fused epilogues (forward z / h,
+# backward dz) beat hipBLASLt + the stand-alone SwiGLU kernels, forward + backward together (tools/gemm_nt_bench.py).
+# Empty: at the 7B shape (22016, 4096) the fused backward is 1.2-1.4 % faster but the fused forward 1.5 % slower,
+# net +0.03 ms per layer (profiles/gemm_nt_swiglu_bwd_pipelined_r4.log)
+NT_FUSED_MLP: set[tuple[int, int]] = set()
+
+
+def nt_fused_mlp_enabled(a: torch.Tensor, wgu: torch.Tensor) -> bool:
+    """Whether the SwiGLU MLP on ``a`` with gate/up weights ``wgu`` ([2F, H]) runs as the fused NT-kernel node
+    (policy as ``nt_enabled``, own shape table ``NT_FUSED_MLP``; the node's plain GEMMs still follow ``nt_enabled``)."""
+    if _NT_MODE == "0" or not (a.is_cuda and a.dim() == 2 and a.dtype == wgu.dtype == torch.bfloat16):
+        return False
+    if _NT_MODE != "1" and (int(wgu.shape[0]), int(wgu.shape[1])) not in NT_FUSED_MLP:
+        return False
+    return bool(ext().gemm_nt_ok(a, wgu))
+
+
 def nt_enabled(a: torch.Tensor, b: torch.Tensor) -> bool:
     """Whether ``a @ b^T`` (2-D, b = [N, K]) runs on the HIP NT kernel (policy above + the kernel's tiling)."""
     if _NT_MODE == "0" or not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2):
