@@ -87,7 +87,7 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
     p.add_argument("--launch-timeout", type=float, default=3000.0, help="launcher: kill all ranks after this many s")
-    return apply_preset(p.parse_args(argv))
+    return apply_preset(p.parse_args(argv), sys.argv[1:] if argv is None else argv)
 
 
 # BASELINE.json configs 3-5 (the 8-GPU layouts; any N the layout divides).  Values override the corresponding flags.
@@ -106,10 +106,28 @@ PRESETS: dict[str, dict[str, Any]] = {
 }
 
 
-def apply_preset(a: argparse.Namespace) -> argparse.Namespace:
-    """Overrides the layout flags of ``a`` with its ``--preset`` (if any) and checks that the GPU count fits."""
+def _explicit_flags(argv: list[str]) -> set[str]:
+    """Destinations of the options given on the command line (``--micro-batch 2`` / ``--micro-batch=2``)."""
+    out = set()
+    for tok in argv:
+        if tok.startswith("--"):
+            out.add(tok[2:].split("=", 1)[0].replace("-", "_"))
+    return out
+
+
+def apply_preset(a: argparse.Namespace, argv: Optional[list[str]] = None) -> argparse.Namespace:
+    """Overrides the layout flags of ``a`` with its ``--preset`` (if any) and checks that the GPU count fits.
+
+    A flag given explicitly on the command line that the preset sets to a different value is an error: the run would
+    otherwise report the preset's name for a layout that was not the one requested."""
     if a.preset is None:
         return a
+    given = _explicit_flags(argv or [])
+    clash = sorted(k for k, v in PRESETS[a.preset].items() if k in given and getattr(a, k) != v)
+    if clash:
+        raise SystemExit(f"bench.py: --preset {a.preset} sets " +
+                         ", ".join(f"--{k.replace('_', '-')}={PRESETS[a.preset][k]}" for k in clash) +
+                         "; drop the conflicting flag(s) or the preset")
     for k, v in PRESETS[a.preset].items():
         setattr(a, k, v)
     if a.gpus % (a.tp * a.pp) != 0:
@@ -410,6 +428,9 @@ def _worker(a: argparse.Namespace) -> None:
                 "seq_len": a.seq_len,
                 "parallelism": parallelism,
                 "preset": a.preset,
+                # the effective layout (after --preset), field by field
+                "tp": a.tp, "pp": a.pp, "dp": dp, "sequence_parallel": a.sequence_parallel,
+                "activation_checkpointing": a.activation_checkpointing, "zero": bool(a.zero),
                 "micro_batch": a.micro_batch,
                 "grad_acc": a.grad_acc,
                 "loss": None if last is None else last.loss,

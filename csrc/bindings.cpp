@@ -460,7 +460,7 @@ bool gemm_tn_ok(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
     return sa_launch::gemm_tn_supported(A.size(1), B.size(1), A.size(0), A.stride(0), B.stride(0), C.stride(0));
 }
 void gemm_tn(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool accumulate) {
-    TORCH_CHECK(gemm_tn_ok(A, B, C), "gemm_tn: unsupported operands (bf16 2-D, M/N multiple of 256, K of 64)");
+    TORCH_CHECK(gemm_tn_ok(A, B, C), "gemm_tn: unsupported operands (bf16 2-D, M/N multiples of 16, K of 128)");
     const at::DeviceGuard g(A.device());
     static int slots = -1;  // one 256x256 tile per CU
     if (slots < 0) {
@@ -636,8 +636,10 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
     if (rope) {
         TORCH_CHECK(rope_sin.has_value() && rope_cos->scalar_type() == at::kFloat && rope_sin->scalar_type() == at::kFloat &&
                     rope_cos->is_contiguous() && rope_sin->is_contiguous() && rope_cos->size(-1) == rope_dim / 2 &&
-                    (!rope_pos.has_value() || (rope_pos->scalar_type() == at::kLong && rope_pos->numel() == T)),
-                    "fa_bwd: rope tables / positions");
+                    (!rope_pos.has_value() ||
+                     (rope_pos->scalar_type() == at::kLong && rope_pos->numel() == T && rope_pos->is_contiguous() &&
+                      rope_pos->device() == q.device())),
+                    "fa_bwd: rope tables / positions (contiguous fp32 tables, contiguous int64 positions of [T])");
         // NeoX pairs sit in one lane for a full rotation (partner accumulator t + D/64), interleaved pairs in one
         // 4-element group; with the dK head split the partials are summed in fa_bwd_reduce_kernel, which does not rotate
         fold = D >= 64 && (rope_interleaved ? rope_dim <= D && rope_dim % 8 == 0 : rope_dim == D) && a.hsplit == 1 &&

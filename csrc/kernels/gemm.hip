@@ -15,8 +15,11 @@
 //  * grid: XCD-aware bijective remap, then 8-row groups of tiles so the 32 tiles resident on one XCD share A/B panels
 //    in its L2; the ragged last round of tiles runs split over K (fp32 partials + a combine pass);
 //  * epilogue: C = acc (+ C) with one bf16 rounding (beta = 1 accumulates into a main-grad buffer).
-// Shapes this kernel does not tile (M/N not multiples of 256, K not a multiple of 128) run on hipBLASLt
-// (scaling_amd/ops/gemm.py).  The pipeline variants measured against this one (ping-pong 8-wave, 2-stage BK 64,
+// Ragged M / N (multiples of 16, e.g. the tensor-parallel shards 5504 = 21.5 x 256, 2752, 16000): the edge tiles load
+// past the last row / column like full ones -- those bytes are either another row of the same operand (only the
+// output rows / columns past M / N see them) or past the buffer resource's byte range, which the LDS-DMA reads as
+// zeros -- and the epilogue stores only the 16 x 16 accumulator blocks inside C (wave-uniform tests).  Shapes this kernel
+// does not tile (M/N not multiples of 16, K not a multiple of 128) run on hipBLASLt (scaling_amd/ops/gemm.py).  The pipeline variants measured against this one (ping-pong 8-wave, 2-stage BK 64,
 // interleaved, register-staged, other ring schedules) are in git history before commit "Delete losing GEMM variants"
 // with their A/B logs in profiles/gemm_variants_*.log and profiles/gemm_ring_variants_r3*.log.
 // Reference op: the weight gradient of F.linear at src/scaling/core/nn/linear/column_parallel_linear.py:151.
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
     // tile coordinates.  Blocks [0, full_blocks) own whole tiles (XCD remap over them); with a split tail the
     // remaining tiles run as tail_split K-slices each (one block per slice) writing fp32 partials that
     // gemm_tn_combine_kernel adds into C: the last round is full instead of ragged.
-    const int tm = M / 256, tn = N / 256;
+    const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     int v, k_lo = 0, nk = K / 64, unit = -1;  // 64-deep tiles (the split plan's unit)
     if ((int)blockIdx.x < full_blocks) {
         v = xcd_remap(blockIdx.x, full_blocks);
@@ -245,16 +248,20 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
         }
         return;
     }
+    const bool edge = m0 + 256 > M || n0 + 256 > N;  // ragged last tile row / column: store the blocks inside C
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+        if (edge && m0 + 128 * wm + 16 * i >= M) continue;  // wave-uniform (M % 16 == 0)
         u16* crow_p = C + (int64_t)(m0 + 128 * wm + 16 * i + r) * ldc + n0 + 128 * wn + q4;
         u16x4 old[8];
         if (BETA) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
+            for (int j = 0; j < 8; ++j)
+                if (!edge || n0 + 128 * wn + 16 * j < N) old[j] = *reinterpret_cast<const u16x4*>(crow_p + 16 * j);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            if (edge && n0 + 128 * wn + 16 * j >= N) continue;
             u16x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -276,7 +283,7 @@ template __global__ void gemm_tn_ring_kernel<false>(const u16* __restrict__, int
 // tail tile v (>= full_blocks): C[m0 + r][n0 + c] = (beta ? C : 0) + sum of its K-slice partials; block (tile, 4 rows)
 __global__ __launch_bounds__(256) void gemm_tn_combine_kernel(const float* __restrict__ ws, u16* __restrict__ C, int ldc,
                                                               int M, int N, int full_blocks, int split, int beta) {
-    const int tm = M / 256, tn = N / 256;
+    const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int v = full_blocks + (int)blockIdx.x;
     const int group = kGroupM * tn;
     const int first_m = (v / group) * kGroupM;
@@ -284,6 +291,7 @@ __global__ __launch_bounds__(256) void gemm_tn_combine_kernel(const float* __res
     const int within = v % group;
     const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
     const int row = 4 * (int)blockIdx.y + (threadIdx.x >> 6), col = (threadIdx.x & 63) * 4;
+    if (m0 + row >= M || n0 + col >= N) return;  // ragged edge tile
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     const float* wp = ws + (int64_t)blockIdx.x * split * 65536 + row * 256 + col;
     for (int p = 0; p < split; ++p) {
@@ -303,7 +311,7 @@ using namespace sa_gemm;
 
 namespace sa_launch {
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
-    return M % 256 == 0 && N % 256 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 &&
+    return M % 16 == 0 && N % 16 == 0 && K % 128 == 0 && M > 0 && N > 0 && K > 0 && lda % 8 == 0 &&
            ldb % 8 == 0 && ldc % 4 == 0 && K * lda * 2 < (int64_t(1) << 31) && K * ldb * 2 < (int64_t(1) << 31) &&
            ldc < (1 << 30);
 }
@@ -312,7 +320,7 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
 // (2..4, >= 4 64-deep tiles per slice and an even number of them, chosen to minimise the tail's rounds x slice
 // length) and a combine pass adds the fp32 partials into C.  Returns the fp32 workspace floats needed (0: no split).
 int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_blocks, int& split) {
-    const int nwg = (int)((M / 256) * (N / 256));
+    const int nwg = (int)(((M + 255) / 256) * ((N + 255) / 256));
     full_blocks = nwg;
     split = 1;
     if (slots <= 0) return 0;
@@ -333,7 +341,7 @@ int64_t gemm_tn_plan(int64_t M, int64_t N, int64_t K, int slots, int& full_block
 }
 void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
              int64_t K, bool beta, hipStream_t st, int full_blocks, int split, float* ws) {
-    const int nwg = (int)((M / 256) * (N / 256));
+    const int nwg = (int)(((M + 255) / 256) * ((N + 255) / 256));
     if (full_blocks < 0 || split <= 1) { full_blocks = nwg; split = 1; }
     const int grid = full_blocks + (nwg - full_blocks) * split;
     const uint32_t ab = (uint32_t)(K * lda * 2), bb = (uint32_t)(K * ldb * 2);

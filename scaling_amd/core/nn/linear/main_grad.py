@@ -55,7 +55,10 @@ from ....ops.gemm import mm_nt, transpose2d, wgrad
 from ...utils.debug_env import side_streams_enabled
 
 _GEN = [0]
-_WT_ENABLED = os.environ.get("SCALING_AMD_DGRAD_WT", "1") != "0"
+_WT_MODE = os.environ.get("SCALING_AMD_DGRAD_WT", "1")
+_WT_ENABLED = _WT_MODE != "0"
+# "all": also small weights (< 1M elements), so every tiling dgrad runs dY (W^T)^T on the NT GEMM path (forensics)
+_WT_MIN_NUMEL = 0 if _WT_MODE == "all" else (1 << 20)
 
 
 _WGRAD_STREAM_ENABLED = os.environ.get("SCALING_AMD_WGRAD_STREAM", "0") == "1"
@@ -108,7 +111,7 @@ def _transposed(weights: Sequence[torch.Tensor], w: torch.Tensor) -> Optional[to
     """Cached contiguous ``w^T`` ([K, sum N]) for the dgrad GEMM, or None where it does not pay."""
     if not (_WT_ENABLED and w.is_cuda and w.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2):
         return None
-    if w.shape[0] % 64 or w.shape[1] % 64 or w.numel() < (1 << 20):
+    if w.shape[0] % 64 or w.shape[1] % 64 or w.numel() < _WT_MIN_NUMEL:
         return None
     key = weights[0]
     c = getattr(key, "_sa_wt_cache", None)

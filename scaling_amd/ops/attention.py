@@ -268,7 +268,7 @@ def rope_flash_attention(base: torch.Tensor, q: torch.Tensor, k: torch.Tensor, v
             return None
     specs = (_spec(q, base), _spec(k, base), _spec(v, base))
     cq = cu_seqlens.to(torch.int32)
-    p = None if pos is None else pos.reshape(-1).long()
+    p = None if pos is None else pos.reshape(-1).long().contiguous()
     win = -1 if window is None else int(window)
     seed = dropout_seed(base.device) if dropout_p > 0.0 else 0
     return _RopeFlashAttn.apply(base, specs, cos, sin, p, int(rot_dim), int(seq_len), bool(interleaved), cq, cq,

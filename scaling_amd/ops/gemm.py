@@ -1,12 +1,15 @@
 """Linear-layer GEMMs on the hand-written gfx950 kernels.
 
-``wgrad``: the weight gradient ``dW (+)= dY^T X`` (``csrc/kernels/gemm.hip``).
+``wgrad``: the weight gradient ``dW (+)= dY^T X`` (``csrc/kernels/gemm.hip``, ``gemm_tn_ring_kernel``).
 
-Both operands arrive token-major (``dY: [T, N]``, ``X: [T, K]``), i.e. k-strided for this product; the
-kernel stages them as they lie (LDS-DMA) and builds MFMA fragments with the transposing LDS read, in a
-ping-pong schedule.  At the 7B layer shapes it runs 1.05-1.25 PF vs hipBLASLt's 0.95-1.2 PF
-(``profiles/gemm_wgrad_r1.log``).  Shapes it does not tile (M/N not multiples of 256, T not a multiple
-of 64) use ``torch.matmul`` / ``addmm_`` (hipBLASLt).
+Both operands arrive token-major (``dY: [T, N]``, ``X: [T, K]``), i.e. k-strided for this product; the kernel stages
+them as they lie (LDS-DMA into a four-slot ring of 32-deep k-steps) and builds MFMA fragments with the transposing LDS
+read, one wave per SIMD, 256 x 256 tiles, 16x16x32 MFMAs accumulating in AGPRs, a split-K tail for the ragged last
+round of tiles.  At the 7B layer shapes it runs 1.43-1.55 PF (MFMA util 0.80-0.81, ``profiles/pmc_step_r4.txt``) where
+hipBLASLt runs this TN layout at 0.95-1.2 PF.  M / N need only be multiples of 16: the tensor-parallel shards 5504,
+2752 and 16000 run in HIP too (ragged edge tiles, ``SCALING_AMD_WGRAD_RAGGED=0`` sends them to hipBLASLt as before
+round 5).  Shapes it does not tile (M/N not multiples of 16, T not a multiple of 128) use ``torch.matmul`` /
+``addmm_`` (hipBLASLt).
 
 ``linear`` is the forward ``x W^T (+ b)`` of every linear layer and ``mm_nt`` the input gradient ``dY (W^T)^T`` on
 the cached transpose: at most 4 token rows (token-by-token decoding) run the weight-streaming GEMV kernel
@@ -25,11 +28,15 @@ import torch
 from ._ext import ext, use_native
 
 
+_WGRAD_RAGGED = os.environ.get("SCALING_AMD_WGRAD_RAGGED", "1") != "0"
+
+
 def wgrad(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
     """``out (+)= dy^T @ x`` for 2-D ``dy [T, N]``, ``x [T, K]``; returns ``out`` ([N, K])."""
     if use_native(dy):
         o = out if out is not None else torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=dy.dtype)
-        if ext().gemm_tn_ok(dy, x, o):
+        ragged = dy.shape[1] % 256 != 0 or x.shape[1] % 256 != 0
+        if (_WGRAD_RAGGED or not ragged) and ext().gemm_tn_ok(dy, x, o):
             ext().gemm_tn(dy, x, o, bool(accumulate and out is not None))
             return o
     if out is None:

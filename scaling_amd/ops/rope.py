@@ -64,6 +64,6 @@ def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: Optio
     """x: [T, heads, head_dim]; pos: [T] absolute positions or None (position = t % seq_len)."""
     if use_native(x):
         if pos is not None:
-            pos = pos.reshape(-1).long()
+            pos = pos.reshape(-1).long().contiguous()
         return _Rope.apply(x, cos, sin, pos, rot_dim, seq_len, interleaved)
     return rope_reference(x, cos, sin, pos, rot_dim, seq_len, interleaved)

@@ -150,14 +150,33 @@ def disable_all() -> None:
         _REGISTRY[group] = None
 
 
+def _world_max(v: int) -> int:
+    """MAX of ``v`` over the whole world (every rank calls this at the same point), ``v`` without a process group."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return v
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([v], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
 def raise_on_errors() -> None:
-    """Host check of the error words (one small device read): raises RuntimeError and retires the communicators if
-    a one-shot all-reduce timed out since the last check.  For forward-only paths; training checks per step."""
-    errs = pending_error_words()
-    if not errs:
+    """Host check of the error words: raises RuntimeError and retires the communicators if a one-shot all-reduce
+    timed out since the last check, on EVERY rank.  For forward-only paths; training checks per step.
+
+    A timeout is often one-sided: the rank that waited sets its word while the late peer saw every flag and finished
+    normally.  Deciding on the local word alone would retire the communicator on one rank only, and the two ranks
+    would then disagree on the all-reduce path (one on RCCL, one in the one-shot kernel): the next TP all-reduce
+    hangs.  So the summed word is MAX all-reduced over the world (as ``Optimizer._grad_stats`` does for training)
+    and every rank resets, retires and raises together.  All ranks reach this call at the same point (end of an
+    evaluation step / ``run_instructions``); with the path disabled by the environment (same on every rank) it
+    costs nothing."""
+    if not enabled():
         return
-    if int(torch.stack(errs).sum().item()) > 0:
+    errs = pending_error_words()
+    local = int(torch.stack(errs).sum().item()) if errs else 0
+    if _world_max(local) > 0:
         reset_error_words()
         disable_all()
-        raise RuntimeError("one-shot tensor-parallel all-reduce timed out waiting for a peer; its outputs were "
-                           "poisoned (NaN); the one-shot path is disabled, RCCL is used from here on")
+        raise RuntimeError("one-shot tensor-parallel all-reduce timed out waiting for a peer on some rank; its outputs "
+                           "were poisoned (NaN); the one-shot path is disabled on every rank, RCCL is used from here on")

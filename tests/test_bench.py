@@ -104,6 +104,19 @@ def test_bench_preset_layouts(preset, gpus, tp, pp, dp, acc, ac, sp, lora):
         bench._args(["--gpus", "1", "--preset", "baseline4"])
 
 
+def test_bench_preset_rejects_conflicting_flags():
+    """An explicit layout flag that the preset would silently overwrite is an error; one that agrees is fine."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    with pytest.raises(SystemExit, match="micro-batch"):
+        bench._args(["--gpus", "8", "--preset", "baseline4", "--micro-batch", "2"])
+    with pytest.raises(SystemExit, match="tp"):
+        bench._args(["--gpus", "8", "--preset", "baseline3", "--tp=4"])
+    a = bench._args(["--gpus", "8", "--preset", "baseline4", "--micro-batch", "4", "--steps", "3"])
+    assert a.micro_batch == 4 and a.steps == 3
+
+
 def test_bench_preset_runs_gloo():
     """The TP2 x PP2 preset (BASELINE #4) end to end on 4 CPU ranks; the JSON names the preset."""
     r = _run(["--gpus", "4", "--preset", "baseline4", "--model", "llama_tiny", "--backend", "gloo", "--seq-len", "64",

@@ -3,6 +3,8 @@ EVERY rank falls back to RCCL (no rank spins on IPC flags while another uses the
 that were allocated / opened are released on every rank."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from tests.dist_utils import run_distributed
@@ -63,12 +65,14 @@ def test_enablement_succeeds_when_all_ranks_succeed():
     assert all(not r[1] and not r[2] for r in res.values())
 
 
-def test_error_word_raises_and_retires_communicators():
+def test_error_word_raises_and_retires_communicators(monkeypatch):
     """A set error word (a peer timeout) makes ``raise_on_errors`` (forward-only paths) raise, clears the word and
     retires every communicator, so later calls use RCCL instead of the out-of-step one-shot protocol."""
     import pytest
 
     from scaling_amd.parallel import custom_allreduce as ca
+
+    monkeypatch.setenv("SCALING_AMD_CUSTOM_ALLREDUCE", "1")
 
     class _Comm:
         def __init__(self) -> None:
@@ -90,3 +94,40 @@ def test_error_word_raises_and_retires_communicators():
     finally:
         ca._REGISTRY.clear()
         ca._REGISTRY.update(saved)
+
+
+def _one_sided_worker(bad_rank: int):
+    import torch.distributed as dist
+
+    from scaling_amd.parallel import custom_allreduce as ca
+
+    os.environ["SCALING_AMD_CUSTOM_ALLREDUCE"] = "1"
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+
+    class _Comm:
+        def __init__(self) -> None:
+            self.err = torch.zeros(1, dtype=torch.int32)
+
+    c = _Comm()
+    ca._REGISTRY.clear()
+    ca._REGISTRY["tp"] = c
+    ca.raise_on_errors()  # healthy everywhere: no rank raises
+    healthy = ca._REGISTRY["tp"] is c
+    if rank == bad_rank:  # only the rank that waited saw the timeout; its late peer finished normally
+        c.err.fill_(1)
+    raised = False
+    try:
+        ca.raise_on_errors()
+    except RuntimeError:
+        raised = True
+    retired = ca._REGISTRY["tp"] is None
+    dist.destroy_process_group()
+    return healthy, raised, retired, int(c.err.item())
+
+
+def test_one_sided_timeout_retires_communicators_on_every_rank():
+    """A timeout seen by one rank only must still make EVERY rank raise and fall back to RCCL: deciding on the local
+    word would leave the ranks on different all-reduce paths and hang the next TP all-reduce."""
+    res = run_distributed(_one_sided_worker, 2, timeout=120, bad_rank=1)
+    assert all(r == (True, True, True, 0) for r in res.values()), res

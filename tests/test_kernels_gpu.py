@@ -396,6 +396,35 @@ def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0,
         assert err / scl < 3e-2, (err, scl)
 
 
+@pytest.mark.parametrize("lens,Hq,Hk,causal,dtype", [
+    ([1024], 8, 2, True, torch.bfloat16),          # v3 forward: 4 q tiles, diagonal tail per wave
+    ([700, 1300, 513], 4, 2, True, torch.bfloat16),  # ragged segments: partial 256-row tiles, waves with no rows
+    ([640, 900], 4, 1, False, torch.bfloat16),     # non-causal: ragged last key tile through the masked tail
+    ([600], 4, 2, True, torch.float16),
+])
+def test_flash_attention_fwd_v3_shapes(lens, Hq, Hk, causal, dtype):
+    """Sequences of >= 512 tokens at D = 128 take the one-wave-per-SIMD, two-block pipelined forward (v3) against the
+    fp32 reference (forward and, through its LSE, the backward)."""
+    _attn_case(lens, Hq, Hk, 128, causal, dtype=dtype)
+
+
+def test_flash_attention_fwd_v3_growing_max():
+    """Scores that grow along the keys make the running row max move by more than the lazy-rescale threshold in
+    later tiles: the deferred O rescale of both pipelined blocks (applied before the block's next P.V) and of the
+    masked tail must match the fp32 reference."""
+    torch.manual_seed(5)
+    T, Hq, Hk, D = 1536, 4, 2, 128
+    cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
+    q = torch.randn(T, Hq, D, device=DEV, dtype=torch.bfloat16)
+    grow = (1.0 + 6.0 * torch.arange(T, device=DEV, dtype=torch.float32) / T).view(T, 1, 1)
+    k = (torch.randn(T, Hk, D, device=DEV) * grow).to(torch.bfloat16)
+    v = torch.randn(T, Hk, D, device=DEV, dtype=torch.bfloat16)
+    for causal in (True, False):
+        o = attention.flash_attention(q, k, v, cu, cu, T, T, 1 / math.sqrt(D), causal)
+        ref = attention.attention_reference(q.float(), k.float(), v.float(), cu, cu, 1 / math.sqrt(D), causal, -1)
+        torch.testing.assert_close(o.float(), ref, atol=2e-2, rtol=2e-2)
+
+
 def test_flash_attention_rejects_fp32():
     """fp32 q/k/v are refused (flash-attn's contract) instead of being computed in bf16 behind the caller's back."""
     q = torch.randn(64, 2, 64, device=DEV)
@@ -526,6 +555,34 @@ def test_gemm_tn(M, N, K, accumulate):
     torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
     assert not ext().gemm_tn_ok(A[:, :200], B, C[:200])
     assert not ext().gemm_tn_ok(A[:64], B[:64], C)
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("M,N,K", [(5504, 4096, 512), (4096, 5504, 256), (16000, 1024, 256), (2752, 512, 384),
+                                   (272, 144, 128)])
+def test_gemm_tn_ragged(M, N, K, accumulate):
+    """The weight-gradient GEMM at the tensor-parallel per-rank shapes whose M / N are not multiples of 256 (TP2: MLP
+    down projection [4096, 5504], LM head [16000, 4096]; TP4: [2752, .]): edge tiles load past the last row / column
+    and store only the 16 x 16 blocks inside C.  C is surrounded by sentinel memory that must stay untouched."""
+    torch.manual_seed(11)
+    A = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+    B = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    pad = 4096
+    Cbuf = torch.full((M * N + 2 * pad,), 7.0, device=DEV, dtype=torch.bfloat16)
+    C = Cbuf[pad : pad + M * N].view(M, N)
+    C0 = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    C.copy_(C0)
+    assert ext().gemm_tn_ok(A, B, C)
+    ext().gemm_tn(A, B, C, accumulate)
+    ref = A.float().t() @ B.float() + (C0.float() if accumulate else 0)
+    torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
+    assert bool((Cbuf[:pad] == 7.0).all()) and bool((Cbuf[pad + M * N :] == 7.0).all())
+    # the framework entry point takes the HIP kernel for these shapes (no hipBLASLt fallback)
+    from scaling_amd.ops import gemm as gemm_ops
+
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    gemm_ops.wgrad(A, B, out)
+    torch.testing.assert_close(out.float(), A.float().t() @ B.float(), atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2),
