@@ -77,6 +77,12 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
                    help="BASELINE.json layouts: baseline3 = TP2 x DP(N/2) ZeRO-1 + SP, baseline4 = TP2 x PP2 x DP(N/4) "
                         "1F1B + activation checkpointing + SP, baseline5 = LoRA TP1 x DP(N) ZeRO-1 (overrides the "
                         "layout flags it names; see PRESETS)")
+    p.add_argument("--shard-proxy", type=str, default=None, choices=["baseline3", "baseline4"],
+                   help="1-GPU per-rank proxy of an 8-GPU preset: ONE process runs rank 0's tensor-parallel shard "
+                        "(TP2: 16 q / 4 kv heads, SwiGLU 5504, vocab 16000) of one pipeline stage's layers (baseline4: "
+                        "16) with the preset's micro-batching, sequence parallelism and checkpointing; collectives are "
+                        "stubbed (core/topology/stub_collectives.py), so the number is per-rank compute, not the "
+                        "headline")
     p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo", "gloo-gpu"],
                    help="gloo = CPU processes (plumbing mode, no GPU); gloo-gpu = rehearsal: GPU ranks (several "
                         "may share one GPU) with gloo collectives standing in for RCCL")
@@ -87,7 +93,8 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--gemm-tuning-out", type=str, default=None)
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
     p.add_argument("--launch-timeout", type=float, default=3000.0, help="launcher: kill all ranks after this many s")
-    return apply_preset(p.parse_args(argv), sys.argv[1:] if argv is None else argv)
+    argv = sys.argv[1:] if argv is None else argv
+    return apply_shard_proxy(apply_preset(p.parse_args(argv), argv), argv)
 
 
 # BASELINE.json configs 3-5 (the 8-GPU layouts; any N the layout divides).  Values override the corresponding flags.
@@ -113,6 +120,27 @@ def _explicit_flags(argv: list[str]) -> set[str]:
         if tok.startswith("--"):
             out.add(tok[2:].split("=", 1)[0].replace("-", "_"))
     return out
+
+
+def apply_shard_proxy(a: argparse.Namespace, argv: Optional[list[str]] = None) -> argparse.Namespace:
+    """``--shard-proxy P``: P's layout for rank 0 of its tensor-parallel group, one pipeline stage, no data parallelism,
+    in one process with the stubbed ("fake") process group.  Explicit --micro-batch / --grad-acc /
+    --activation-checkpointing flags win (the A/B of checkpointing modes at the per-rank shape)."""
+    if a.shard_proxy is None:
+        return a
+    lay = PRESETS[a.shard_proxy]
+    given = _explicit_flags(argv or [])
+    for k in ("micro_batch", "grad_acc", "sequence_parallel", "tp_comm_chunks", "lora", "zero",
+              "activation_checkpointing"):
+        if k not in given:
+            setattr(a, k, lay[k])
+    a.tp, a.pp = lay["tp"], 1
+    if a.num_layers is None:
+        from scaling_amd.models import llama_architecture
+
+        a.num_layers = llama_architecture(a.model)["num_layers"] // lay["pp"]
+    a.gpus = a.tp
+    return a
 
 
 def apply_preset(a: argparse.Namespace, argv: Optional[list[str]] = None) -> argparse.Namespace:
@@ -250,6 +278,8 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
     if a.backend in ("gloo", "gloo-gpu"):
         topo["backend"] = "gloo"
         topo["gloo_on_gpu"] = a.backend == "gloo-gpu"
+    if a.shard_proxy is not None:
+        topo["backend"] = "fake"
     return {
         "topology": topo,
         "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero),
@@ -285,6 +315,8 @@ def _worker(a: argparse.Namespace) -> None:
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local = _env_int("LOCAL_RANK", 0)
+    if a.shard_proxy is not None:  # one process = rank 0 of the TP group (stubbed collectives)
+        world, rank, local = a.gpus, 0, 0
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -343,6 +375,26 @@ def _worker(a: argparse.Namespace) -> None:
 
         optimizer.step = traced_step
 
+    # race-check forensics: the gradient ENTERING every module's backward, in backward execution order, as stream-ordered
+    # device checksums (no host sync inside the step): the first entry where two runs differ names the module whose
+    # successor (in forward order) produced a different input gradient
+    gtrace: list = []
+    if trace and os.environ.get("SCALING_AMD_BENCH_TRACE_GRADS") == "1":
+        def _grad_probe(name: str) -> Any:
+            def fwd_hook(_m: Any, _inp: Any, out: Any) -> None:
+                ts = [out] if torch.is_tensor(out) else [t for t in (out if isinstance(out, (tuple, list)) else [])
+                                                           if torch.is_tensor(t)]
+                ts += [v for v in (getattr(out, "__dict__", {}) or {}).values() if torch.is_tensor(v)]
+                for i, t in enumerate(ts):
+                    if t.requires_grad and t.is_floating_point():
+                        t.register_hook(lambda g, n=f"{name}[{i}]": gtrace.append(
+                            (n, torch.stack([g.double().sum(), (g.double() * g.double()).sum()]))))
+            return fwd_hook
+
+        for mname, mod in model.named_modules():
+            if mname:
+                mod.register_forward_hook(_grad_probe(mname))
+
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,
                                metrics_aggregation_fn)
@@ -357,7 +409,9 @@ def _worker(a: argparse.Namespace) -> None:
                        # local (pre-reduction) gradients: lazy zeroing leaves them in the flat buffer after the step
                        "pgrads": [float(p.grad.double().sum()) if p.grad is not None else None
                                   for p in model.parameters()],
-                       "pgrads_pre": pre[0].tolist() if pre else []}
+                       "pgrads_pre": pre[0].tolist() if pre else [],
+                       "gtrace": [(n, [float(x) for x in v.tolist()]) for n, v in gtrace]}
+            gtrace.clear()
             with open(f"{trace}.rank{rank}.jsonl", "a") as f:
                 f.write(json.dumps(rec) + "\n")
         n_steps[0] += 1
@@ -399,18 +453,26 @@ def _worker(a: argparse.Namespace) -> None:
     ms = 1000.0 * sec / a.steps
     if rank == 0:
         headline = (a.num_layers is None and a.model == "llama2_7b" and a.seq_len == 4096 and a.backend == "auto"
-                    and a.precision == "bfloat16")
+                    and a.precision == "bfloat16" and a.shard_proxy is None)
         flops_tok = 6 * unique_params + 12 * arch["num_layers"] * arch["hidden_size"] * a.seq_len
         if a.lora:  # frozen base: no weight-gradient GEMMs for the base weights (~1/3 of the 6N)
             flops_tok = None
         parallelism = (f"tp{a.tp}_pp{a.pp}_dp{dp}" + ("_zero1" if a.zero else "") +
                        (f"_ac-{a.activation_checkpointing}" if a.activation_checkpointing != "disabled" else "") +
                        ("_sp" if a.sequence_parallel else "") + ("_lora" if a.lora else ""))
+        proxy_est = None
+        if a.shard_proxy is not None:
+            world_note = (f"per-rank proxy of --preset {a.shard_proxy}: rank 0 of TP{a.tp}, {arch['num_layers']} layers "
+                          "(one pipeline stage), collectives stubbed; value = ONE rank's tokens/s")
+            lay = PRESETS[a.shard_proxy]
+            # what 8 GPUs of the preset would reach with free communication: 8 / (tp pp) data-parallel replicas, each
+            # pipeline running at the 1F1B efficiency m / (m + pp - 1) (m micro-batches)
+            proxy_est = (tokens / sec) * 8 / (lay["tp"] * lay["pp"]) * a.grad_acc / (a.grad_acc + lay["pp"] - 1)
         res = {
-            "metric": METRIC,
+            "metric": METRIC if a.shard_proxy is None else "per-rank proxy tokens/s (NOT the headline): " + world_note,
             "value": tokens / sec,
             "unit": "tokens/s",
-            "n_gpus": world,
+            "n_gpus": world if a.shard_proxy is None else 1,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms,
@@ -428,6 +490,8 @@ def _worker(a: argparse.Namespace) -> None:
                 "seq_len": a.seq_len,
                 "parallelism": parallelism,
                 "preset": a.preset,
+                "shard_proxy": a.shard_proxy,
+                "proxy_8gpu_tokens_s_without_comm": proxy_est,
                 # the effective layout (after --preset), field by field
                 "tp": a.tp, "pp": a.pp, "dp": dp, "sequence_parallel": a.sequence_parallel,
                 "activation_checkpointing": a.activation_checkpointing, "zero": bool(a.zero),
@@ -472,7 +536,7 @@ def main() -> None:
         # the LoRA path's GEMMs write / read column slices (ld > n): TunableOp's tuning pass mis-handles them
         # (invalid-argument errors and non-finite results measured on MI355X); tune on the full-training path
         raise SystemExit("bench.py: --gemm-tuning tune is not supported with --lora")
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1 and a.shard_proxy is None:
         sys.exit(_launch(a))
     _worker(a)
 

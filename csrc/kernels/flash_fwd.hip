@@ -462,6 +462,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     tv.init(wave, lane, a.v_tok);
     const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
+    const uint32_t lds0 = lds_addr(smem);
 
     // Q of the whole workgroup (256 rows) lives in LDS after the K/V ring (64 KiB; 160 KiB in all): in registers the two
     // blocks' fragments would take 64 VGPRs that the softmax of two blocks needs.  Row qwg0 + r sits at image row r, so
@@ -469,8 +470,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     {
         DmaTile<D, C::NW, C::BM> tq;
         tq.init(wave, lane, a.q_tok);
-        dma_load(tq, a.q + (int64_t)(q0s + qwg0) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qwg0,
-                 smem + C::QOFF, wave);
+        dma_load_asm(tq, a.q + (int64_t)(q0s + qwg0) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qwg0,
+                     lds0 + C::QOFF, wave);
     }
     int qoff[C::NKS];
 #pragma unroll
@@ -502,7 +503,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     // file, which keeps the arch VGPRs for S, Q, P and the fragments (with compiler MFMAs the allocator shuffles 2 x 64
     // O registers through v_accvgpr copies and spills).  The asm is invisible to the hazard recognizer: P is written by
     // VALU (v_cvt_pk) and read as SrcB, which needs 2 wait states, so the first MFMA of every P register carries
-    // s_nop 1; readers of O (rescale, epilogue) sit behind o_fence.
+    // s_nop 1 -- "first" in program order, which asm volatile pins (non-volatile asm MFMAs of different accumulators
+    // were reordered so that a t > 0 MFMA read a fresh P without the pad: rare wrong outputs); readers of O (rescale,
+    // epilogue) sit behind o_fence.
     auto pv = [&](f32x16 (&o)[C::NT], const bf16x8 (&p)[2][2], const char* V) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < C::NT; ++t)
@@ -515,11 +518,11 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
                     const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
                     const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
                     if (t == 0) {
-                        if constexpr (F16) asm("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
-                        else asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
+                        if constexpr (F16) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
+                        else asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
                     } else {
-                        if constexpr (F16) asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
-                        else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
+                        if constexpr (F16) asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
+                        else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(o[t]) : "v"(vf), "v"(p[b][ss]));
                     }
                 }
     };
@@ -603,12 +606,18 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     };
 
     const int ntiles = (khi + C::KT - 1) / C::KT;
-    auto issue = [&](int t, char* slot) __attribute__((always_inline)) {
+    // K/V tile t into ring slot `cs` (asm LDS-DMA: waited for by the s_waitcnt vmcnt(0) in front of the next tile's
+    // barrier, a whole tile later)
+    auto issue = [&](int t, int cs) __attribute__((always_inline)) {
         const int kt = t * C::KT;
-        dma_load(tk, kbase + (int64_t)kt * a.k_tok, a.k_tok, Lk - kt, slot, wave);
-        dma_load(tv, vbase + (int64_t)kt * a.v_tok, a.v_tok, Lk - kt, slot + C::TILE, wave);
+        dma_load_asm(tk, kbase + (int64_t)kt * a.k_tok, a.k_tok, Lk - kt, lds0 + cs * C::SLOT, wave);
+        dma_load_asm(tv, vbase + (int64_t)kt * a.v_tok, a.v_tok, Lk - kt, lds0 + cs * C::SLOT + C::TILE, wave);
     };
-    if (ntiles > 0) issue(0, smem);
+    auto tile_barrier = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    if (ntiles > 0) issue(0, 0);
 
     // one pipelined tile (no mask for either block).  PEND: block B's tile t-1 is still in flight (the steady state);
     // a compile-time flag, so no branch splits a phase's MFMAs from the filler work scheduled beside them
@@ -634,6 +643,9 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
         pv(oA, pA, K + C::TILE);
         smax(sB, mB, lB, alB, needB);
         sexp(sB, mB, rsB, 0);
+        // keep block B's first-half exps in this phase: without a use here hipcc sinks them below the next tile's
+        // barrier into phase 1, which then carries twice its share of VALU beside the same 16 MFMAs
+        asm volatile("" : "+v"(sB[0]), "+v"(rsB[0]), "+v"(rsB[1]), "+v"(rsB[2]), "+v"(rsB[3]));
         pend = true;
     };
 
@@ -643,8 +655,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     const int nmain = max(0, min(a.causal ? (qwg0 + off + 1) / C::KT : ntiles, Lk / C::KT));
     auto head = [&](auto cslot, int t) __attribute__((always_inline)) {
         constexpr int CS = decltype(cslot)::value;
-        __syncthreads();  // tile t landed (every wave waited for its own pieces); slot of tile t-2 is free
-        if (t + 1 < ntiles) issue(t + 1, smem + ((CS + 1) % 3) * C::SLOT);
+        tile_barrier();  // tile t landed (every wave waited for its own pieces); slot of tile t-2 is free
+        if (t + 1 < ntiles) issue(t + 1, (CS + 1) % 3);
     };
     auto mtile = [&](auto cslot, auto pendc, int t) __attribute__((always_inline)) {
         constexpr int CS = decltype(cslot)::value;
@@ -671,8 +683,8 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
     // others as serial masked steps (runtime slot addresses: a few tiles per workgroup)
     for (; t < ntiles; ++t) {
         const int cs = t % 3;
-        __syncthreads();
-        if (t + 1 < ntiles) issue(t + 1, smem + ((cs + 1) % 3) * C::SLOT);
+        tile_barrier();
+        if (t + 1 < ntiles) issue(t + 1, (cs + 1) % 3);
         const int kt = t * C::KT;
         if (kt < khw) {
             const char* K = smem + cs * C::SLOT;

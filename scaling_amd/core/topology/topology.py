@@ -85,7 +85,7 @@ class Topology:
     # ------------------------------------------------------------------ init
     def initialize_device(self) -> None:
         rehearsal = self.config.backend == "gloo" and self.config.gloo_on_gpu
-        if torch.cuda.is_available() and (self.config.backend != "gloo" or rehearsal):
+        if torch.cuda.is_available() and (self.config.backend != "gloo" or rehearsal):  # incl. "fake" (per-rank proxy)
             slot = self.config.local_slot if self.config.local_slot is not None else 0
             if rehearsal:
                 slot %= torch.cuda.device_count()
@@ -116,6 +116,12 @@ class Topology:
         )
         backend = self.config.backend or ("nccl" if self.device.type == "cuda" else "gloo")
         self.backend = backend
+        if backend == "fake" and not dist.is_initialized():  # per-rank proxy: one process, stubbed collectives
+            from .stub_collectives import init_fake_process_group, install as install_stubs
+
+            assert self.config.pipe_parallel_size == 1, "the stubbed process group cannot run a pipeline"
+            init_fake_process_group(self.config.world_size, self.config.global_rank)
+            install_stubs()
         if not dist.is_initialized():
             kwargs: dict[str, Any] = dict(
                 backend=backend,

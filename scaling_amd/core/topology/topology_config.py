@@ -94,7 +94,8 @@ class TopologyConfig(BaseConfig):
     backend: Optional[str] = Field(
         None,
         description="torch.distributed backend; None selects 'nccl' (RCCL over xGMI) when a GPU is "
-        "present and 'gloo' otherwise",
+        "present and 'gloo' otherwise; 'fake' = one process playing rank global_rank with stubbed collectives "
+        "(the per-rank compute proxy, core/topology/stub_collectives.py)",
     )
     gloo_on_gpu: bool = Field(
         False,

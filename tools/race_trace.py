@@ -39,7 +39,8 @@ def main():
     out = os.path.join(ROOT, "gpurun_out", "race_trace")
     os.makedirs(out, exist_ok=True)
     env = {"SCALING_AMD_SINGLE_STREAM": os.environ.get("SCALING_AMD_SINGLE_STREAM", "1"),
-           "SCALING_AMD_DETERMINISTIC": "1"}
+           "SCALING_AMD_DETERMINISTIC": "1",
+           "SCALING_AMD_BENCH_TRACE_GRADS": os.environ.get("SCALING_AMD_BENCH_TRACE_GRADS", "1")}
     runs = int(os.environ.get("RACE_TRACE_RUNS", "2"))
     for i in range(runs):
         for r in range(gpus):
@@ -52,7 +53,17 @@ def main():
             a, b = load(os.path.join(out, "run0"), r), load(os.path.join(out, f"run{k}"), r)
             first = None
             for x, y in zip(a, b):
-                for key in ("loss", "pgrads_pre", "pgrads", "grads", "grad_norm", "params"):
+                for key in ("loss", "gtrace", "pgrads_pre", "pgrads", "grads", "grad_norm", "params"):
+                    if key not in x:
+                        continue
+                    if key == "gtrace" and x[key] != y[key]:
+                        idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
+                        j0 = idx[0]
+                        first = (x["step"], f"gtrace: first differing input gradient #{j0} of {len(x[key])} "
+                                 f"(backward order) entering {x[key][j0][0]}: {x[key][j0][1]} vs {y[key][j0][1]}; "
+                                 f"previous entries: {[e[0] for e in x[key][max(0, j0 - 3):j0]]}",
+                                 x["loss"], y["loss"])
+                        break
                     if x[key] != y[key]:
                         diff = key
                         if isinstance(x[key], list):
