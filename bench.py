@@ -394,6 +394,9 @@ def _worker(a: argparse.Namespace) -> None:
         for mname, mod in model.named_modules():
             if mname:
                 mod.register_forward_hook(_grad_probe(mname))
+        from scaling_amd.core.utils import grad_probe
+
+        grad_probe.enable(gtrace)  # + the probes inside the layers (attention input / q,k,v / core output, layer input)
 
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,

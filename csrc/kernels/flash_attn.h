@@ -172,6 +172,16 @@ __device__ __forceinline__ void dma_load_asm(const DmaTile<D, W, R>& t, const vo
                              ::"s"(l), "v"(t.voff[i]), "s"(rs) : "m0");
         }
 }
+// Workgroup barrier after which every wave may read what ANY wave staged by LDS-DMA: each wave first waits for its own
+// pieces (s_waitcnt vmcnt(0)), then the barrier.  A plain __syncthreads() is not enough inside a loop: hipcc emits only
+// lgkmcnt(0) there and puts the vmcnt wait in front of the wave's next ds_read, which covers only its OWN pieces -- a
+// wave could read a slower peer's piece of the next tile before it landed (the stale bytes of two tiles ago).  That
+// happened rarely, under load (cdna_hip_programming.md §5 "Read a staged buffer one phase AFTER the wait that retires
+// it"; found by the race check's gradient trace, tools/race_trace.py).
+__device__ __forceinline__ void dma_barrier() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((const lds_void*)p));
 }

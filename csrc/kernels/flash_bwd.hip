@@ -359,21 +359,21 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         issue(ig, iq, buf0);
         adv(ig, iq);
     }
-    __syncthreads();
+    dma_barrier();
     int w = 0;
     for (; w + 1 < nwork; w += 2) {
         issue(ig, iq, buf1);
         adv(ig, iq);
         tile(buf0, cg, cq);
         adv(cg, cq);
-        __syncthreads();
+        dma_barrier();  // every wave's pieces of the next work item landed (see dma_barrier)
         if (w + 2 < nwork) {
             issue(ig, iq, buf0);
             adv(ig, iq);
         }
         tile(buf1, cg, cq);
         adv(cg, cq);
-        __syncthreads();
+        dma_barrier();
     }
     if (w < nwork) tile(buf0, cg, cq);
 
@@ -532,16 +532,16 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     char* buf0 = smem;
     char* buf1 = smem + 2 * TILE;
     if (klo < khi) SA_DQ_ISSUE(klo, buf0);
-    __syncthreads();
+    dma_barrier();
     const int ntiles = khi > klo ? (khi - klo + 63) / 64 : 0;
     int kt = klo;
     for (int pr = 0; pr < ntiles / 2; ++pr, kt += 128) {
         SA_DQ_ISSUE(kt + 64, buf1);
         tile(buf0, kt);
-        __syncthreads();
+        dma_barrier();  // every wave's pieces of tile kt + 64 landed (see dma_barrier)
         if (kt + 128 < khi) SA_DQ_ISSUE(kt + 128, buf0);
         tile(buf1, kt + 64);
-        __syncthreads();
+        dma_barrier();
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_DQ_ISSUE

@@ -365,17 +365,17 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     char* buf0 = smem;
     char* buf1 = smem + 2 * C::TILE;
     if (klo < khi) SA_FWD_ISSUE(klo, buf0);
-    __syncthreads();
+    dma_barrier();
     // pairs of tiles (buffer 0 then 1) so every LDS address is register + immediate; odd tail peeled
     const int ntiles = khi > klo ? (khi - klo + C::KT - 1) / C::KT : 0;
     int kt = klo;
     for (int pr = 0; pr < ntiles / 2; ++pr, kt += 2 * C::KT) {
         SA_FWD_ISSUE(kt + C::KT, buf1);
         tile(buf0, kt);
-        __syncthreads();
+        dma_barrier();  // every wave's pieces of tile kt + KT landed (see dma_barrier)
         if (kt + 2 * C::KT < khi) SA_FWD_ISSUE(kt + 2 * C::KT, buf0);
         tile(buf1, kt + C::KT);
-        __syncthreads();
+        dma_barrier();
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_FWD_ISSUE
@@ -613,10 +613,7 @@ __global__ __launch_bounds__(256, 1) void fa_fwd_v3_kernel(FwdArgs a) {
         dma_load_asm(tk, kbase + (int64_t)kt * a.k_tok, a.k_tok, Lk - kt, lds0 + cs * C::SLOT, wave);
         dma_load_asm(tv, vbase + (int64_t)kt * a.v_tok, a.v_tok, Lk - kt, lds0 + cs * C::SLOT + C::TILE, wave);
     };
-    auto tile_barrier = [&]() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
+    auto tile_barrier = [&]() __attribute__((always_inline)) { dma_barrier(); };
     if (ntiles > 0) issue(0, 0);
 
     // one pipelined tile (no mask for either block).  PEND: block B's tile t-1 is still in flight (the steady state);

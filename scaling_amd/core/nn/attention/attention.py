@@ -33,6 +33,7 @@ from ..lora_config import LoRaConfig, LoRAModuleType
 from ..masked_softmax import MaskedSoftmax, MaskedSoftmaxConfig, MaskedSoftmaxKernel
 from ..norm import LayerNorm, LayerNormConfig, NormType, RMSNorm, get_norm
 from ..rotary import RotaryConfig, RotaryEmbedding, RotaryEmbeddingComplex
+from ...utils.grad_probe import probe
 
 
 class RelativePositionEmbeddingType(Enum):
@@ -578,6 +579,7 @@ class ParallelSelfAttention(torch.nn.Module):
         T = b * s
         hd = self.hidden_size_per_attention_head
         fused_append: Optional[tuple] = None
+        probe("attention.input", x)
         if projected_step is not None:  # graph decode: norm + q/k/v GEMV + RoPE + K/V append were one launch
             q, k, v, cumulative_seq_lengths_key = projected_step
             fused_append = projected_step
@@ -591,11 +593,12 @@ class ParallelSelfAttention(torch.nn.Module):
             lora_in_base = lora_pending and self._lora_into_base(x, base)
             if lora_in_base:  # fresh views of the updated GEMM output
                 q, k, v = self._views(base, T)
+            probe("attention.qkv", base)
             if not use_cache and not reset_cache and cumulative_seq_lengths_key is None:
                 fused = self._fused_rope_attention(base, q, k, v, position_ids, s, cumulative_seq_lengths, max_seq_length,
                                                    lora_in_base=lora_in_base)
                 if fused is not None:
-                    return self._output(fused.reshape(b, s, -1))
+                    return self._output(probe("attention.core", fused).reshape(b, s, -1))
             if lora_pending and not lora_in_base:
                 q, k, v = self.apply_lora(x, q, k, v)
             if self.key_query_norm:

@@ -7,14 +7,15 @@ real layout runs, while the collectives between the ranks are replaced by local 
 head split, HIP vs vendor kernel routing, activation checkpointing cost) is measurable on one GPU; communication time
 is not in it.
 
-``fake``'s own semantics: all-reduce and broadcast leave the tensor unchanged, all-gather writes the local input into
-every rank's slot.  Its reduce-scatter leaves the output unwritten (uninitialised memory): ``install`` makes it copy
-this rank's slice of the input instead.  Point-to-point messages have no peer, so pipeline parallelism is refused.
+``install`` replaces every collective this framework calls by a local stand-in with the semantics of a group whose
+ranks all hold this rank's data: all-reduce / broadcast / barrier do nothing, all-gather replicates the local input
+into every slot, reduce-scatter copies this rank's slice of the input (torch's ``fake`` backend only provides the
+process-group plumbing; on GPU tensors it leaves outputs unwritten, which made the first proxy run diverge to NaN).
+Point-to-point messages have no peer, so pipeline parallelism is refused.
 """
 from __future__ import annotations
 
-import functools
-from typing import Any, Callable
+from typing import Any
 
 import torch
 import torch.distributed as dist
@@ -28,14 +29,49 @@ def init_fake_process_group(world_size: int, rank: int) -> None:
     dist.init_process_group("fake", store=FakeStore(), world_size=world_size, rank=rank)
 
 
-def _wrap_reduce_scatter(orig: Callable[..., Any]) -> Callable[..., Any]:
-    @functools.wraps(orig)
-    def fn(output: torch.Tensor, input: torch.Tensor, op: Any = None, group: Any = None, async_op: bool = False) -> Any:
-        r, n = dist.get_rank(group), output.numel()
-        output.view(-1).copy_(input.reshape(-1)[r * n:(r + 1) * n])
-        return None
+class _Done:
+    def wait(self, timeout: Any = None) -> bool:
+        return True
 
-    return fn
+    def is_completed(self) -> bool:
+        return True
+
+
+def _ret(async_op: bool) -> Any:
+    return _Done() if async_op else None
+
+
+# Local stand-ins with the tensor semantics of a group whose every rank holds this rank's data (stream-ordered torch
+# ops on the current stream; torch's fake backend is not relied on for writing outputs).
+def _all_reduce(tensor: torch.Tensor, op: Any = None, group: Any = None, async_op: bool = False) -> Any:
+    return _ret(async_op)
+
+
+def _broadcast(tensor: torch.Tensor, src: Any = None, group: Any = None, async_op: bool = False, **_k: Any) -> Any:
+    return _ret(async_op)
+
+
+def _all_gather_into_tensor(output: torch.Tensor, input: torch.Tensor, group: Any = None, async_op: bool = False) -> Any:
+    n = dist.get_world_size(group)
+    output.view(n, -1).copy_(input.reshape(1, -1).expand(n, -1))
+    return _ret(async_op)
+
+
+def _all_gather(tensor_list: list, tensor: torch.Tensor, group: Any = None, async_op: bool = False) -> Any:
+    for t in tensor_list:
+        t.copy_(tensor)
+    return _ret(async_op)
+
+
+def _reduce_scatter_tensor(output: torch.Tensor, input: torch.Tensor, op: Any = None, group: Any = None,
+                           async_op: bool = False) -> Any:
+    r, n = dist.get_rank(group), output.numel()
+    output.view(-1).copy_(input.reshape(-1)[r * n:(r + 1) * n])
+    return _ret(async_op)
+
+
+def _barrier(group: Any = None, async_op: bool = False, **_k: Any) -> Any:
+    return _ret(async_op)
 
 
 def _refuse_p2p(*_a: Any, **_k: Any) -> Any:
@@ -44,12 +80,17 @@ def _refuse_p2p(*_a: Any, **_k: Any) -> Any:
 
 
 def install() -> None:
-    """Idempotent: local reduce-scatter semantics, p2p refused."""
+    """Idempotent: every collective this framework calls gets its local stand-in, p2p is refused."""
     global _installed
     if _installed:
         return
     _installed = True
-    dist.reduce_scatter_tensor = _wrap_reduce_scatter(dist.reduce_scatter_tensor)
+    dist.all_reduce = _all_reduce
+    dist.broadcast = _broadcast
+    dist.all_gather_into_tensor = _all_gather_into_tensor
+    dist.all_gather = _all_gather
+    dist.reduce_scatter_tensor = _reduce_scatter_tensor
+    dist.barrier = _barrier
     dist.batch_isend_irecv = _refuse_p2p
     dist.isend = _refuse_p2p
     dist.irecv = _refuse_p2p

@@ -1,0 +1,32 @@
+"""Race-check forensics: stream-ordered checksums of the gradients flowing through named points of the backward.
+
+``enable(records)`` turns probing on: every ``probe(name, t)`` on a tensor that requires grad then registers a hook
+that appends ``(name, tensor([sum, sum of squares]))`` (float64, on the device, no host sync) to ``records`` when the
+backward reaches ``t``, so ``records`` lists the gradients in backward execution order.  Two runs that should be
+bit-identical are compared entry by entry (``tools/race_trace.py``): the first differing entry names the op that ran
+between it and the previous entry.  Off (the default) ``probe`` is a dictionary lookup."""
+from __future__ import annotations
+
+from typing import Any, Optional
+
+import torch
+
+_records: Optional[list] = None
+
+
+def enable(records: list) -> None:
+    global _records
+    _records = records
+
+
+def disable() -> None:
+    global _records
+    _records = None
+
+
+def probe(name: str, t: Any) -> Any:
+    rec = _records
+    if rec is not None and torch.is_tensor(t) and t.requires_grad and t.is_floating_point():
+        t.register_hook(lambda g, n=name: rec.append(
+            (n, torch.stack([g.double().sum(), (g.double() * g.double()).sum()]))))
+    return t

@@ -11,7 +11,8 @@ from ...data.inference_settings import InferenceSettings
 
 class TransformerLayerIO(BaseLayerIO):
     _FIELDS = ("activations", "position_ids", "cumulative_seq_lengths", "cumulative_seq_lengths_padded",
-               "loss_weights", "inference_settings", "embeddings", "embeddings_head", "attention_scores_manipulation")
+               "loss_weights", "inference_settings", "embeddings", "embeddings_head", "attention_scores_manipulation",
+               "residual_branch")
 
     @staticmethod
     def field_names() -> list[str]:
@@ -38,8 +39,13 @@ class TransformerLayerIO(BaseLayerIO):
         embeddings: Optional[torch.Tensor] = None,
         embeddings_head: Optional[torch.Tensor] = None,
         attention_scores_manipulation: Optional[torch.Tensor] = None,
+        residual_branch: Optional[torch.Tensor] = None,
     ) -> None:
         self.activations = activations
+        # a transformer layer may hand over its hidden state as (activations, residual_branch) with the MLP's residual
+        # add still pending: the next layer's input norm does that add inside its kernel (one HBM pass and one launch
+        # less per layer); every consumer takes ``hidden()`` or the add-norm
+        self.residual_branch = residual_branch
         self.position_ids = position_ids
         self.cumulative_seq_lengths = cumulative_seq_lengths
         self.cumulative_seq_lengths_padded = cumulative_seq_lengths_padded
@@ -52,8 +58,15 @@ class TransformerLayerIO(BaseLayerIO):
         self.vocab_parallel: Optional[tuple[int, Any, int]] = None
         self.max_seq_length: Optional[int] = None
 
+    def hidden(self) -> torch.Tensor:
+        """The hidden state with a pending residual add applied."""
+        if self.residual_branch is None:
+            return self.activations
+        return self.activations + self.residual_branch
+
     def derive(self, activations: torch.Tensor, **overrides: Any) -> "TransformerLayerIO":
         kw = {n: getattr(self, n) for n in self._FIELDS}
+        kw["residual_branch"] = None  # a pending add belongs to the activations it came with
         kw.update(activations=activations, **overrides)
         out = TransformerLayerIO(**kw)
         out.max_seq_length = self.max_seq_length

@@ -9,6 +9,7 @@ from typing import Callable, Optional, Union
 import torch
 
 from ....core import ParallelMLP, ParallelSelfAttention, ParallelSwiGLUMLP, RotaryConfig, Topology, get_norm
+from ....core.utils.grad_probe import probe
 from ....ops.elementwise import dropout_add
 from ...context.config import MLPType, TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
@@ -18,6 +19,9 @@ from .embedding import _device
 _DECODE_FUSED = os.environ.get("SCALING_AMD_DECODE_FUSED", "1") != "0"
 # decode-sized RMSNorms as prologues of the following GEMVs; SCALING_AMD_DECODE_NORM_GEMV=0 for A/B
 _DECODE_NORM_GEMV = _DECODE_FUSED and os.environ.get("SCALING_AMD_DECODE_NORM_GEMV", "1") != "0"
+# hand the MLP's residual add to the next layer's add-norm kernel (TransformerLayerIO.residual_branch);
+# SCALING_AMD_DEFER_RESIDUAL=0 for A/B
+_DEFER_RESIDUAL = os.environ.get("SCALING_AMD_DEFER_RESIDUAL", "1") != "0"
 
 
 class ZeroLayer(torch.nn.Module):
@@ -144,24 +148,30 @@ class TransformerLayer(TransformerLayerBaseIO):
     def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
         st = x.inference_settings
         assert x.cumulative_seq_lengths is not None
-        attn_args = (x.activations, x.cumulative_seq_lengths, x.position_ids,
+        pending = probe(f"layer{self.layer_index}.branch_in", x.residual_branch)  # the previous layer's MLP output,
+        probe(f"layer{self.layer_index}.input", x.activations)                # its residual add not done yet
+        decode_step = _DECODE_NORM_GEMV and st is not None and st.use_cache and not st.reset_cache
+        fused_path = (self.dropout_attention.p == 0.0 or not self.training) and not hasattr(self, "attn_adapter_name")
+        hidden = x.activations if (pending is None or (fused_path and not decode_step)) else x.hidden()
+        attn_args = (hidden, x.cumulative_seq_lengths, x.position_ids,
                      st.use_cache if st else False, st.reset_cache if st else False, st.cache_index if st else 0,
                      x.attention_scores_manipulation, st.control_log_additive_batch if st else True)
-        if (self.dropout_attention.p == 0.0 or not self.training) and not hasattr(self, "attn_adapter_name"):
-            # residual stream through the fused norms: input_layernorm folds the residual-branch gradient into its
-            # backward; post_attention_layernorm writes x + attn and norm(x + attn) in one pass
+        capture = st is not None and (self.layer_index + 1) in st.embedding_layers
+        if fused_path:
+            # residual stream through the fused norms: input_layernorm adds the previous layer's pending MLP output
+            # (or, without one, folds the residual-branch gradient into its backward); post_attention_layernorm writes
+            # x + attn and norm(x + attn) in one pass
             # (decode-sized rows: both norms run as prologues of the q/k/v and gate/up GEMVs instead)
             # only on real decode steps (a cached step after the prompt): the fold keeps the normalised row in fp32, so
             # a short prompt, eval or scoring batch must take the same norm + GEMM path as any longer input
-            decode_step = _DECODE_NORM_GEMV and st is not None and st.use_cache and not st.reset_cache
             proj = getattr(self.self_attention, "decode_norm_project", None) if decode_step else None
-            kw = proj(x.activations, self.input_layernorm, attn_args[2], attn_args[3], attn_args[4],
+            kw = proj(hidden, self.input_layernorm, attn_args[2], attn_args[3], attn_args[4],
                       attn_args[5]) if proj is not None else None
             if kw is None:
                 kw = {}
-                resid, normed = self.input_layernorm.forward_add(x.activations, None)
+                resid, normed = self.input_layernorm.forward_add(hidden, pending if hidden is x.activations else None)
             else:
-                resid = normed = x.activations
+                resid = normed = hidden
             h = self.self_attention(
                 normed, cumulative_seq_lengths=attn_args[1], position_ids=attn_args[2], use_cache=attn_args[3],
                 reset_cache=attn_args[4], cache_index=attn_args[5], attention_scores_manipulation=attn_args[6],
@@ -173,10 +183,14 @@ class TransformerLayer(TransformerLayerBaseIO):
                 act = fused(h, resid, self.post_attention_layernorm) if fused is not None else None
             if act is None:
                 resid, normed = self.post_attention_layernorm.forward_add(resid, h)
+                if (_DEFER_RESIDUAL and not decode_step and not capture and not hasattr(self, "mlp_adapter_name")
+                        and (self.dropout_mlp.p == 0.0 or not self.training)):
+                    # leave resid + mlp(normed) to the next layer's add-norm (or the final norm)
+                    return x.derive(resid, embeddings_head=None, residual_branch=self.mlp(normed))
                 act = self._mlp_tail(resid, normed)
         else:
             act = self.mlp_block(self.attention_block(*attn_args))
-        if st is not None and (self.layer_index + 1) in st.embedding_layers:
+        if capture:
             assert x.embeddings is not None
             x.embeddings[st.embedding_layers.index(self.layer_index + 1)] = act
         return x.derive(act, embeddings_head=None)

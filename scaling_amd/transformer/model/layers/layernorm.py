@@ -20,7 +20,10 @@ class LayerNormWrapper(TransformerLayerBaseIO):
         self.layer_index = layer_index
 
     def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
-        act = self.norm(x.activations)
+        if x.residual_branch is not None and hasattr(self.norm, "forward_add"):  # last layer's pending MLP residual add
+            act = self.norm.forward_add(x.activations, x.residual_branch)[1]
+        else:
+            act = self.norm(x.hidden())
         st = x.inference_settings
         if st is not None and (self.layer_index + 1) in st.embedding_layers:
             assert x.embeddings is not None

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import json
+import math
 import os
 import subprocess
 import sys
@@ -143,3 +144,21 @@ def test_default_tp_comm_chunks():
     assert a.tp_comm_chunks == 0  # resolved when the config is built
     cfg = bench._config_dict(a, 2, 0, 0)
     assert cfg["topology"]["tensor_parallel_comm_chunks"] == a.tp_comm_chunks >= 2
+
+
+@pytest.mark.parametrize("preset,ac", [("baseline3", None), ("baseline4", "every_layer_save_matmuls")])
+def test_bench_shard_proxy_gloo(preset, ac):
+    """``--shard-proxy``: one process runs rank 0's TP2 shard of the preset (one pipeline stage's layers) with stubbed
+    collectives; the JSON says it is a per-rank proxy (not the headline), on one device, with the preset's layout
+    (an explicit --activation-checkpointing wins for the checkpointing A/B)."""
+    args = ["--shard-proxy", preset, "--model", "llama_tiny", "--backend", "gloo", "--seq-len", "64", "--steps", "1",
+            "--warmup", "1"] + (["--activation-checkpointing", ac] if ac else [])
+    r = _run(args, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _json_lines(r.stdout)[0]
+    assert res["metric"].startswith("per-rank proxy") and res["n_gpus"] == 1 and res["vs_baseline"] is None
+    c = res["config"]
+    assert c["shard_proxy"] == preset and c["tp"] == 2 and c["pp"] == 1 and c["dp"] == 1 and c["sequence_parallel"]
+    assert c["activation_checkpointing"] == (ac or ("every_layer" if preset == "baseline4" else "disabled"))
+    assert c["micro_batch"] == (4 if preset == "baseline4" else 8) and math.isfinite(c["loss"])
+    assert c["proxy_8gpu_tokens_s_without_comm"] > 0

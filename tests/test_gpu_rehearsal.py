@@ -107,27 +107,19 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         (["--gpus", "1", "--backend", "auto"], {}),                            # overlapped step on its side stream
         (["--gpus", "1", "--backend", "auto"], {"SCALING_AMD_WGRAD_STREAM": "1"}),  # + weight-gradient stream
         (["--gpus", "2"], {}),                                                 # DP comm stream
-        pytest.param(["--gpus", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"},  # ... running 1 ms late per collective
-                     marks=pytest.mark.xfail(strict=False, reason=(
-                         "open: under the 1 ms delay the multi-stream runs are not repeatable among themselves: the "
-                         "local gradients of the last layers of the backward differ while the forward loss is "
-                         "bit-identical, on hipBLASLt sporadically and with rocBLAS in every run, while single-stream "
-                         "runs repeat bit for bit (profiles/race_trace_r4.log, README 'Race check')"))),
-        pytest.param(["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"},
-                     marks=pytest.mark.xfail(strict=False, reason="as the DP2 delayed case")),
-        pytest.param(["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {},
-                     marks=pytest.mark.xfail(strict=False, reason=(
-                         "open: with 8 ranks on the one GPU even the single-stream twin does not repeat bit for bit "
-                         "(pipeline stage-0 gradients of the first layer / embedding differ between single-stream "
-                         "runs, loss identical: profiles/race_trace_world8_r4.log), so the comparison has no fixed "
-                         "reference"))),
+        (["--gpus", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),              # ... running 1 ms late per collective
+        (["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),
+        (["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {}),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):
     """Race check: the multi-stream schedule (DP communication stream, overlapped optimizer step,
     optional weight-gradient stream, per-layer event waits) must leave bit-identical parameters and losses to
     the same run with every side stream folded onto the compute stream (SCALING_AMD_SINGLE_STREAM=1).  A missing
-    stream / event dependency shows up as a different checksum.  Both runs use library-side determinism
+    stream / event dependency shows up as a different checksum -- and so does any kernel whose result depends on
+    timing: the delayed and 8-rank cases were xfail in round 4 until the gradient trace (tools/race_trace.py, probes
+    in core/utils/grad_probe.py) pinned their divergence on the attention backward, whose loop barriers did not retire
+    every wave's LDS-DMA pieces of the next tile (flash_attn.h: dma_barrier; tools/dma_barrier_check.py).  Both runs use library-side determinism
     (SCALING_AMD_DETERMINISTIC=1: torch deterministic algorithms, rocBLAS without atomics): with several ranks sharing
     the one GPU, the default vendor GEMM kernels' atomic accumulation order varies from run to run even with every
     stream folded (profiles/race_repeat_dp2_r4.log), which would hide what this test checks."""
