@@ -143,35 +143,6 @@ __device__ __forceinline__ void dma_load(const DmaTile<D, W, R>& t, const void* 
     t.load(base, tok, rows, tile, wave_u);
 }
 
-// The same tile load issued by inline asm (cdna_hip_programming.md §5 item 4(b)): a compiler-visible LDS-DMA makes
-// hipcc's waitcnt pass put s_waitcnt vmcnt(0) in front of the next ds_read of ANY LDS address (it cannot tell which
-// bytes are pending), which drains a tile-ahead prefetch one phase after it was issued.  The caller owns the wait:
-// s_waitcnt vmcnt(N) + a barrier before the first read of the tile.  m0 is written in the statement that uses it.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4 rsrc_words(const void* p, uint32_t nbytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(p);
-    return i32x4{(int)__builtin_amdgcn_readfirstlane((uint32_t)a),
-                 (int)(__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) & 0xffff),
-                 (int)__builtin_amdgcn_readfirstlane(nbytes), kBufFlags};
-}
-template <int D, int W, int R>
-__device__ __forceinline__ void dma_load_asm(const DmaTile<D, W, R>& t, const void* base, int64_t tok, int rows,
-                                             uint32_t lds_tile, int wave_u) {
-    const i32x4 rs = rsrc_words(base, (uint32_t)max(rows, 0) * (uint32_t)tok * 2u);
-#pragma unroll
-    for (int i = 0; i < DmaTile<D, W, R>::NPW; ++i)
-        if (DmaTile<D, W, R>::PIECES >= W || wave_u + W * i < DmaTile<D, W, R>::PIECES) {
-            const uint32_t l = lds_tile + (uint32_t)(wave_u + W * i) * 1024u;
-            // the first piece carries the 5 wait states after the v_readfirstlane writes of the descriptor SGPRs
-            // inside the statement that reads them (a separate s_nop statement could be scheduled before them)
-            if (i == 0)
-                asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                             ::"s"(l), "v"(t.voff[i]), "s"(rs) : "m0");
-            else
-                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                             ::"s"(l), "v"(t.voff[i]), "s"(rs) : "m0");
-        }
-}
 // Workgroup barrier after which every wave may read what ANY wave staged by LDS-DMA: each wave first waits for its own
 // pieces (s_waitcnt vmcnt(0)), then the barrier.  A plain __syncthreads() is not enough inside a loop: hipcc emits only
 // lgkmcnt(0) there and puts the vmcnt wait in front of the wave's next ds_read, which covers only its OWN pieces -- a
@@ -181,9 +152,6 @@ __device__ __forceinline__ void dma_load_asm(const DmaTile<D, W, R>& t, const vo
 __device__ __forceinline__ void dma_barrier() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-}
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>((const lds_void*)p));
 }
 
 // 3-way max without the canonicalising v_max the compiler wraps around fmaxf

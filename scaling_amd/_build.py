@@ -84,10 +84,8 @@ def _check_kernel_stubs(so: Path) -> None:
         raise RuntimeError("kernel host stubs missing from the extension:\n" + "\n".join(missing))
 
 
-# per-file device flags.  flash_fwd.hip: the one-wave-per-SIMD forward (fa_fwd_v3_kernel) keeps its O accumulators in
-# AGPRs by inline asm; without this flag hipcc then also selects the AGPR form for the compiler-visible S = K Q^T MFMAs
-# and copies every S tile back to VGPRs for the softmax (32 v_accvgpr_read per phase, tools/isa_hist.py)
-_FILE_FLAGS = {"flash_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# per-file device flags (source file name -> extra hipcc flags); none needed at present
+_FILE_FLAGS: dict[str, list[str]] = {}
 
 
 def _compile(src: Path, flags: list[str]) -> Path:

@@ -26,6 +26,7 @@ from ....ops._ext import ext, use_native
 from ...topology import Topology
 from ..linear import ColumnParallelLinear, RowParallelLinear
 from ..linear.fused import fused_column_linear
+from ..linear.tp_overlap import sp_gather_column
 from ..linear.utils import all_concat, all_reduce_scatter_to_sequence_parallel, all_shard
 from ..linear.main_grad import adjacent_weights, invalidate_transposed_weights
 from ..lora import ParallelLoRa
@@ -401,6 +402,23 @@ class ParallelSelfAttention(torch.nn.Module):
             return qkv[..., :hd], qkv[..., hd : 2 * hd], qkv[..., 2 * hd :]
         return self._views(base, T)
 
+    def sp_shard_eligible(self) -> bool:
+        """Whether ``project_sp_shard`` applies: sequence parallelism over more than one rank and no unmerged LoRA
+        adapters (they read the gathered input)."""
+        if self.topology is None or not self.topology.config.sequence_parallel:
+            return False
+        if self.topology.config.model_parallel_size < 2 or (self.lora_config is not None and not self.lora_merged_state):
+            return False
+        return True
+
+    def project_sp_shard(self, x: torch.Tensor) -> torch.Tensor:
+        """The q/k/v projection of the sequence-parallel token shard ``x`` ([b, s/tp, h]) with its all-gather folded
+        into the GEMM and overlapped (``tp_overlap.sp_gather_column``): ``[b, s, (heads + 2 kv heads) hd / tp]``, to be
+        passed to ``forward`` as ``projected_base``."""
+        mods = [self.query_key_value] if self.qkv_in_one else [self.query, self.key, self.value]
+        biases = [getattr(m, "bias_param", None) for m in mods]
+        return sp_gather_column(x, [m.weight for m in mods], biases, self.topology)
+
     def decode_norm_project(self, x: torch.Tensor, norm: torch.nn.Module, position_ids: Optional[torch.Tensor] = None,
                             use_cache: bool = False, reset_cache: bool = False, cache_index: int = 0) -> Optional[dict]:
         """The q/k/v projection of ``norm(x)`` for decode-sized inputs (<= 4 tokens, no autograd graph, bias-free,
@@ -575,7 +593,9 @@ class ParallelSelfAttention(torch.nn.Module):
         """``projected_base``: the q/k/v projection of ``x`` already computed; ``projected_step``: (q, k cache,
         v cache, key cu_seqlens) of a graph-decode token whose RoPE and cache append are done
         (both from ``decode_norm_project``)."""
-        b, s, _ = x.shape
+        # a projection computed outside carries the full token shape (x may be a sequence-parallel shard, see
+        # project_sp_shard)
+        b, s = (projected_base.shape[0], projected_base.shape[1]) if projected_base is not None else x.shape[:2]
         T = b * s
         hd = self.hidden_size_per_attention_head
         fused_append: Optional[tuple] = None

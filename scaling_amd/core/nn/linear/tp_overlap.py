@@ -1,4 +1,11 @@
-"""Row-parallel output collectives overlapped with the row-parallel GEMM (TP forward).
+"""Tensor-parallel collectives overlapped with the GEMMs next to them.
+
+``sp_gather_column`` (sequence parallelism, input side): the all-gather of a norm's token shard is folded into the
+column-parallel q/k/v or gate/up GEMM that consumes it -- the GEMM of this rank's own rows runs while the other ranks'
+rows arrive, and in the backward the reduce-scatter of the input gradient runs under the weight-gradient GEMM
+(``_SPGatherColumn``).
+
+``row_parallel_chunked`` (output side): row-parallel output collectives overlapped with the row-parallel GEMM.
 
 A row-parallel linear (attention ``dense``, MLP ``dense_out``) produces partial sums that the TP group must
 all-reduce (or, with sequence parallelism, reduce-scatter over tokens) before anything can use them; the
@@ -28,8 +35,9 @@ import torch
 import torch.distributed as dist
 
 from ....ops.attention import stash_gemm
+from ....ops.gemm import mm_nt
 from ...utils.debug_env import side_streams_enabled
-from .main_grad import _MultiLinear, _transposed, weight_grads
+from .main_grad import _adjacent, _MultiLinear, _rehome_adjacent, _transposed, weight_grads
 
 _streams: dict[int, Any] = {}
 
@@ -163,6 +171,114 @@ def _sp_backward_chunked(ctx: Any, g: torch.Tensor) -> tuple:
     if ctx.needs_input_grad[4]:
         dws = weight_grads(gfull.view(T, N), x.reshape(T, K), [weight], [N])
     return (None if dx is None else dx.view(x.shape), None, None, None, dws[0], None, None, None, None)
+
+
+def _mm_into(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor) -> None:
+    if a.shape[0] == 0:
+        return
+    if b is None:
+        torch.mm(a, w.t(), out=out)
+    else:
+        torch.addmm(b, a, w.t(), out=out)
+
+
+class _SPGatherColumn(torch.autograd.Function):
+    """``all_gather_seq(x) @ [W_1; ...; W_n]^T (+ b)``: the sequence-parallel gather of a norm output folded into the
+    column-parallel GEMM that consumes it, with the collective overlapped both ways.
+
+    Forward: the all-gather of the token shards runs on the TP communication stream while the GEMM of this rank's OWN
+    rows (already local) runs on the compute stream; the other ranks' rows follow once they have arrived.  The gathered
+    input is written where ``gather_from_sequence_parallel_region`` would put it (rank-major flattened tokens), so
+    every output row lands in place: no permutation, no copy, contiguous GEMM operands.  Backward: the input-gradient
+    GEMM over all tokens, then its reduce-scatter (the gather's backward) on the communication stream while the
+    weight-gradient GEMM runs (Megatron's overlapped sequence-parallel backward; the reference runs norm gather, GEMM,
+    and in the backward GEMMs then reduce-scatter back to back: ``core/nn/linear/utils.py:177-192``)."""
+
+    @staticmethod
+    def forward(ctx: Any, x: torch.Tensor, n: int, want_wt: bool, group: Any, size: int, rank: int,  # type: ignore[override]
+                *params: Optional[torch.Tensor]) -> torch.Tensor:
+        weights, biases = params[:n], params[n:]
+        w = _adjacent(weights)
+        if w is None:
+            w = torch.cat(weights, dim=0)  # type: ignore[arg-type]
+        has_bias = len(biases) > 0 and biases[0] is not None
+        b = (biases[0] if n == 1 else torch.cat(biases, dim=0)) if has_bias else None  # type: ignore[arg-type]
+        K = x.shape[-1]
+        Ts = x.numel() // K
+        xs = x.reshape(Ts, K)
+        T, N = Ts * size, w.shape[0]
+        full = torch.empty((T, K), dtype=x.dtype, device=x.device)
+        out = torch.empty((T, N), dtype=x.dtype, device=x.device)
+        cs = _tp_comm_stream(x.device)
+        main = torch.cuda.current_stream(x.device) if cs is not None else None
+        if cs is not None:
+            assert main is not None
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs):
+                dist.all_gather_into_tensor(full, xs, group=group)
+        else:
+            dist.all_gather_into_tensor(full, xs, group=group)
+        _mm_into(xs, w, b, out[rank * Ts : (rank + 1) * Ts])  # own rows: overlaps the gather
+        if cs is not None:
+            assert main is not None
+            main.wait_stream(cs)
+        _mm_into(full[: rank * Ts], w, b, out[: rank * Ts])
+        _mm_into(full[(rank + 1) * Ts :], w, b, out[(rank + 1) * Ts :])
+        wt = _transposed(weights, w) if want_wt else None
+        ctx.has_wt = wt is not None
+        ctx.save_for_backward(full, wt if wt is not None else w, *weights)
+        ctx.n, ctx.has_bias, ctx.group, ctx.size = n, has_bias, group, size
+        ctx.splits = [t.shape[0] for t in weights]  # type: ignore[union-attr]
+        ctx.x_shape = x.shape
+        lead = list(x.shape[:-1])
+        lead[1 if len(lead) > 1 else 0] *= size
+        return out.view(*lead, N)
+
+    @staticmethod
+    def backward(ctx: Any, g: torch.Tensor):  # type: ignore[override]
+        full, w, *weights = ctx.saved_tensors
+        n, size = ctx.n, ctx.size
+        T, K = full.shape
+        g2 = g.reshape(T, g.shape[-1])
+        shard = None
+        cs = _tp_comm_stream(g.device)
+        main = torch.cuda.current_stream(g.device) if cs is not None else None
+        if ctx.needs_input_grad[0]:
+            dx = mm_nt(g2, w) if ctx.has_wt else torch.matmul(g2, w)  # [T, K]
+            shard = torch.empty((T // size, K), dtype=dx.dtype, device=dx.device)
+            if cs is not None:
+                assert main is not None
+                cs.wait_stream(main)
+                with torch.cuda.stream(cs):
+                    dist.reduce_scatter_tensor(shard, dx, group=ctx.group)
+                dx.record_stream(cs)
+            else:
+                dist.reduce_scatter_tensor(shard, dx, group=ctx.group)
+        dws: list[Optional[torch.Tensor]] = [None] * n
+        if any(ctx.needs_input_grad[6 : 6 + n]):
+            dws = weight_grads(g2, full, weights, ctx.splits)  # overlaps the reduce-scatter
+        dbs: list[Optional[torch.Tensor]] = []
+        if ctx.has_bias:
+            gb = g2.sum(0)
+            dbs = list(torch.split(gb, ctx.splits, dim=0)) if n > 1 else [gb]
+        if cs is not None and shard is not None:
+            assert main is not None
+            main.wait_stream(cs)
+        return (None if shard is None else shard.view(ctx.x_shape), None, None, None, None, None, *dws, *dbs)
+
+
+def sp_gather_column(x: torch.Tensor, weights: list, biases: Optional[list], topology: Any) -> torch.Tensor:
+    """``gather_from_sequence_parallel_region(x)`` followed by the column-parallel ``x @ [W_1; ...]^T (+ b)`` of
+    ``weights`` as ONE overlapped node (``_SPGatherColumn``); ``x`` is this rank's sequence-parallel token shard."""
+    size, rank = topology.config.model_parallel_size, topology.model_parallel_rank
+    want_wt = torch.is_grad_enabled() and x.requires_grad
+    if len(weights) > 1 and _adjacent(weights) is None:
+        _rehome_adjacent(weights)
+    if biases is None or any(b is None for b in biases):
+        return _SPGatherColumn.apply(x.contiguous(), len(weights), want_wt, topology.model_parallel_group, size, rank,
+                                     *weights)
+    return _SPGatherColumn.apply(x.contiguous(), len(weights), want_wt, topology.model_parallel_group, size, rank,
+                                 *weights, *biases)
 
 
 def _collective(part: torch.Tensor, dst: Optional[torch.Tensor], group: Any) -> None:

@@ -37,11 +37,13 @@ class RMSNorm(torch.nn.Module):
             out = gather_from_sequence_parallel_region(out, topology=self.topology, tensor_parallel_output_grad=True)
         return out
 
-    def forward_add(self, x: torch.Tensor, res: Optional[torch.Tensor]) -> tuple[torch.Tensor, torch.Tensor]:
+    def forward_add(self, x: torch.Tensor, res: Optional[torch.Tensor], gather: bool = True
+                    ) -> tuple[torch.Tensor, torch.Tensor]:
         """``s = x + res; return s, self(s)`` with the residual add fused into the norm kernel (``res=None``: s = x,
-        the gradient reaching s is added inside the norm backward)."""
+        the gradient reaching s is added inside the norm backward).  ``gather=False``: under sequence parallelism the
+        normalised output stays this rank's token shard (its consumer gathers it, ``tp_overlap.sp_gather_column``)."""
         s, out = norm_ops.add_rms_norm(x, res, self.weight, self.eps)
-        if self.topology is not None and self.topology.config.sequence_parallel:
+        if gather and self.topology is not None and self.topology.config.sequence_parallel:
             out = gather_from_sequence_parallel_region(out, topology=self.topology, tensor_parallel_output_grad=True)
         return s, out
 

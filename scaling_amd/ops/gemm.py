@@ -77,6 +77,23 @@ def nt_fused_mlp_enabled(a: torch.Tensor, wgu: torch.Tensor) -> bool:
     return bool(ext().gemm_nt_ok(a, wgu))
 
 
+# (F, H) down-projection shapes where the backward's dh = dY W_down GEMM with the SwiGLU backward in its epilogue
+# (``gemm_nt_swiglu_bwd``: writes dz, no dh round trip, no stand-alone SwiGLU backward pass) beat hipBLASLt + the
+# SwiGLU backward kernel: 2.576 vs 2.606 ms per 7B layer (profiles/gemm_nt_swiglu_bwd_pipelined_r4.log).  Used with
+# the unfused forward (hipBLASLt gate/up GEMM + SwiGLU kernel), which is faster than the fused one at this shape.
+NT_SWIGLU_BWD: set[tuple[int, int]] = {(11008, 4096)}
+_SWIGLU_BWD_MODE = os.environ.get("SCALING_AMD_SWIGLU_BWD_NT", "auto")
+
+
+def nt_swiglu_bwd_enabled(dy_like: torch.Tensor, wdt_shape: tuple[int, int]) -> bool:
+    """Policy: whether the SwiGLU backward rides on the NT kernel's dz epilogue for dY shaped like ``dy_like`` ([T, H])
+    and ``W_down^T`` of shape ``wdt_shape`` ([F, H]); ``SCALING_AMD_SWIGLU_BWD_NT``: 1 = every shape (the caller still
+    checks that the kernel tiles it, ``gemm_nt_ok``), 0 = never, auto = the shapes in ``NT_SWIGLU_BWD``."""
+    if _SWIGLU_BWD_MODE == "0" or not (dy_like.is_cuda and dy_like.dim() == 2 and dy_like.dtype == torch.bfloat16):
+        return False
+    return _SWIGLU_BWD_MODE == "1" or tuple(wdt_shape) in NT_SWIGLU_BWD
+
+
 def nt_enabled(a: torch.Tensor, b: torch.Tensor) -> bool:
     """Whether ``a @ b^T`` (2-D, b = [N, K]) runs on the HIP NT kernel (policy above + the kernel's tiling)."""
     if _NT_MODE == "0" or not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2):

@@ -10,6 +10,7 @@ import torch
 
 from ....core import ParallelMLP, ParallelSelfAttention, ParallelSwiGLUMLP, RotaryConfig, Topology, get_norm
 from ....core.utils.grad_probe import probe
+from ....ops.attention import stash_active
 from ....ops.elementwise import dropout_add
 from ...context.config import MLPType, TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
@@ -22,6 +23,9 @@ _DECODE_NORM_GEMV = _DECODE_FUSED and os.environ.get("SCALING_AMD_DECODE_NORM_GE
 # hand the MLP's residual add to the next layer's add-norm kernel (TransformerLayerIO.residual_branch);
 # SCALING_AMD_DEFER_RESIDUAL=0 for A/B
 _DEFER_RESIDUAL = os.environ.get("SCALING_AMD_DEFER_RESIDUAL", "1") != "0"
+# sequence parallelism: the norms hand their token shard to the q/k/v and gate/up GEMMs, which gather it overlapped
+# with the GEMM (core/nn/linear/tp_overlap.py: sp_gather_column); SCALING_AMD_SP_OVERLAP=0 gathers in the norms
+_SP_OVERLAP = os.environ.get("SCALING_AMD_SP_OVERLAP", "1") != "0"
 
 
 class ZeroLayer(torch.nn.Module):
@@ -120,13 +124,22 @@ class TransformerLayer(TransformerLayerBaseIO):
             attentions_score_manipulation_log_additive=attentions_score_manipulation_log_additive,
         )
 
-    def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor) -> torch.Tensor:
+    def _sp_overlap(self, decode_step: bool) -> bool:
+        """Whether this forward hands sequence-parallel norm shards to their GEMMs (``_SP_OVERLAP``): TP > 1 with
+        sequence parallelism, a training-shaped step, attention without unmerged LoRA, outside a GEMM-keeping
+        checkpoint region (whose replay would re-run the gather)."""
+        if not _SP_OVERLAP or decode_step or self.topology is None or stash_active():
+            return False
+        return self.self_attention.sp_shard_eligible()
+
+    def _mlp_tail(self, residual: torch.Tensor, normed: torch.Tensor, sp_shard: bool = False) -> torch.Tensor:
         out = None
-        fused = getattr(self.mlp, "decode_forward_residual", None) if _DECODE_FUSED else None
+        fused = getattr(self.mlp, "decode_forward_residual", None) if _DECODE_FUSED and not sp_shard else None
         if fused is not None and (self.dropout_mlp.p == 0.0 or not self.training):
             out = fused(normed, residual)  # decode-sized rows: GEMV epilogues (SwiGLU, residual add)
         if out is None:
-            out = self._dropout_add(self.dropout_mlp, self.mlp(normed), residual)
+            mlp_out = self.mlp(normed, sp_shard=True) if sp_shard else self.mlp(normed)
+            out = self._dropout_add(self.dropout_mlp, mlp_out, residual)
         if hasattr(self, "mlp_adapter_name"):
             out = out + self.apply_adapter(out, self.mlp_adapter_name)
         return out
@@ -167,9 +180,13 @@ class TransformerLayer(TransformerLayerBaseIO):
             proj = getattr(self.self_attention, "decode_norm_project", None) if decode_step else None
             kw = proj(hidden, self.input_layernorm, attn_args[2], attn_args[3], attn_args[4],
                       attn_args[5]) if proj is not None else None
+            sp = kw is None and self._sp_overlap(decode_step)
             if kw is None:
                 kw = {}
-                resid, normed = self.input_layernorm.forward_add(hidden, pending if hidden is x.activations else None)
+                resid, normed = self.input_layernorm.forward_add(hidden, pending if hidden is x.activations else None,
+                                                                 gather=not sp)
+                if sp:  # normed is this rank's token shard: the q/k/v GEMM gathers it, overlapped
+                    kw = {"projected_base": self.self_attention.project_sp_shard(normed)}
             else:
                 resid = normed = hidden
             h = self.self_attention(
@@ -182,12 +199,13 @@ class TransformerLayer(TransformerLayerBaseIO):
                 fused = getattr(self.mlp, "decode_forward_norm", None)
                 act = fused(h, resid, self.post_attention_layernorm) if fused is not None else None
             if act is None:
-                resid, normed = self.post_attention_layernorm.forward_add(resid, h)
+                resid, normed = self.post_attention_layernorm.forward_add(resid, h, gather=not sp)
                 if (_DEFER_RESIDUAL and not decode_step and not capture and not hasattr(self, "mlp_adapter_name")
                         and (self.dropout_mlp.p == 0.0 or not self.training)):
                     # leave resid + mlp(normed) to the next layer's add-norm (or the final norm)
-                    return x.derive(resid, embeddings_head=None, residual_branch=self.mlp(normed))
-                act = self._mlp_tail(resid, normed)
+                    branch = self.mlp(normed, sp_shard=True) if sp else self.mlp(normed)
+                    return x.derive(resid, embeddings_head=None, residual_branch=branch)
+                act = self._mlp_tail(resid, normed, sp_shard=sp)
         else:
             act = self.mlp_block(self.attention_block(*attn_args))
         if capture:

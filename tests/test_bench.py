@@ -82,6 +82,24 @@ def test_bench_tp_comm_chunks_gloo(sp):
     assert losses["2"] == pytest.approx(losses["1"], rel=1e-5)
 
 
+@pytest.mark.parametrize("extra", [[], ["--tp-comm-chunks", "2"], ["--grad-acc", "2", "--gpus", "4", "--pp", "2"]])
+def test_bench_sp_gather_overlap_gloo(extra):
+    """Sequence parallelism with the norm's all-gather folded into (and overlapped with) the q/k/v and gate/up GEMMs
+    (SCALING_AMD_SP_OVERLAP=1, default) trains to the losses and parameters of the gather-in-the-norm path."""
+    losses = {}
+    for mode in ("0", "1"):
+        args = ["--tp", "2", "--sequence-parallel", *TINY, *extra]
+        if "--gpus" not in extra:
+            args = ["--gpus", "2", *args]
+        r = _run(args, env_extra={"SCALING_AMD_SP_OVERLAP": mode})
+        assert r.returncode == 0, r.stderr[-4000:]
+        res = _json_lines(r.stdout)[0]
+        losses[mode] = (res["config"]["loss"], res["config"].get("param_checksum"))
+    assert losses["1"][0] == pytest.approx(losses["0"][0], rel=1e-5)
+    if losses["0"][1] is not None:
+        assert losses["1"][1] == pytest.approx(losses["0"][1], rel=1e-4)
+
+
 @pytest.mark.parametrize("preset,gpus,tp,pp,dp,acc,ac,sp,lora", [
     ("baseline3", 8, 2, 1, 4, 1, "disabled", True, False),
     ("baseline4", 8, 2, 2, 2, 4, "every_layer", True, False),

@@ -397,21 +397,19 @@ def _attn_case(lens, Hq, Hk, D, causal, window=-1, dtype=torch.bfloat16, seed=0,
 
 
 @pytest.mark.parametrize("lens,Hq,Hk,causal,dtype", [
-    ([1024], 8, 2, True, torch.bfloat16),          # v3 forward: 4 q tiles, diagonal tail per wave
-    ([700, 1300, 513], 4, 2, True, torch.bfloat16),  # ragged segments: partial 256-row tiles, waves with no rows
+    ([1024], 8, 2, True, torch.bfloat16),          # 8 q tiles, diagonal tile per wave
+    ([700, 1300, 513], 4, 2, True, torch.bfloat16),  # ragged segments: partial 128-row tiles, waves with no rows
     ([640, 900], 4, 1, False, torch.bfloat16),     # non-causal: ragged last key tile through the masked tail
     ([600], 4, 2, True, torch.float16),
 ])
-def test_flash_attention_fwd_v3_shapes(lens, Hq, Hk, causal, dtype):
-    """Sequences of >= 512 tokens at D = 128 take the one-wave-per-SIMD, two-block pipelined forward (v3) against the
-    fp32 reference (forward and, through its LSE, the backward)."""
+def test_flash_attention_long_ragged_shapes(lens, Hq, Hk, causal, dtype):
+    """Long ragged segments at D = 128 against the fp32 reference (forward and, through its LSE, the backward)."""
     _attn_case(lens, Hq, Hk, 128, causal, dtype=dtype)
 
 
-def test_flash_attention_fwd_v3_growing_max():
+def test_flash_attention_growing_max():
     """Scores that grow along the keys make the running row max move by more than the lazy-rescale threshold in
-    later tiles: the deferred O rescale of both pipelined blocks (applied before the block's next P.V) and of the
-    masked tail must match the fp32 reference."""
+    later tiles: the lazy O rescale (a wave-uniform branch) must match the fp32 reference."""
     torch.manual_seed(5)
     T, Hq, Hk, D = 1536, 4, 2, 128
     cu = torch.tensor([0, T], device=DEV, dtype=torch.int32)
@@ -1074,3 +1072,36 @@ def test_swiglu_mlp_fused_node_matches_unfused(T, H, F, monkeypatch):
         scale = r.abs().max().item()
         assert (a.reshape(r.shape) - r).abs().max().item() < 0.03 * scale
         assert (a - b).abs().max().item() < 0.03 * scale
+
+
+@pytest.mark.parametrize("T,H,F", [(512, 256, 512), (1024, 512, 768)])
+def test_swiglu_down_bwd_epilogue_matches_unfused(T, H, F, monkeypatch):
+    """The unfused forward with the SwiGLU backward on the down projection's dgrad epilogue (``_SwiGLUDown``,
+    SCALING_AMD_SWIGLU_BWD_NT=1) gives the output and every gradient of the all-unfused path to bf16 accuracy."""
+    from scaling_amd.core.nn import mlp as mlp_mod
+    from scaling_amd.ops import gemm as gemm_ops
+
+    torch.manual_seed(4)
+    monkeypatch.setattr(gemm_ops, "_NT_MODE", "0")  # keep the one-node fused MLP out of it
+    mlp = mlp_mod.ParallelSwiGLUMLP(H, F / H, bias=False, device=torch.device(DEV), dtype=torch.bfloat16)
+    x = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
+    calls = []
+    orig = mlp_mod._SwiGLUDown.apply
+    monkeypatch.setattr(mlp_mod._SwiGLUDown, "apply", lambda *a: calls.append(1) or orig(*a))
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(gemm_ops, "_SWIGLU_BWD_MODE", mode)
+        for p in mlp.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        n = len(calls)
+        y = mlp(xi)
+        assert (len(calls) > n) == (mode == "1")
+        y.backward(dy)
+        res[mode] = [y.float(), xi.grad.float()] + [p.grad.float() for p in (mlp.dense_in.weight,
+                                                                              mlp.siglu_weight.weight,
+                                                                              mlp.dense_out.weight)]
+    assert torch.equal(res["1"][0], res["0"][0])  # same forward kernels
+    for a, b in zip(res["1"][1:], res["0"][1:]):
+        assert (a - b).abs().max().item() < 0.03 * b.abs().max().item()

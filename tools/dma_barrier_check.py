@@ -15,8 +15,8 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FILES = {"flash_fwd.hip": ("fa_fwd_v2_kernel", "fa_fwd_v3_kernel"), "flash_bwd.hip": ("fa_bwd_dkdv_kernel", "fa_bwd_dq_kernel")}
-FLAGS = {"flash_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+FILES = {"flash_fwd.hip": ("fa_fwd_v2_kernel",), "flash_bwd.hip": ("fa_bwd_dkdv_kernel", "fa_bwd_dq_kernel")}
+FLAGS: dict = {}
 
 
 def check_file(name: str, kernels: tuple[str, ...]) -> list[str]:
