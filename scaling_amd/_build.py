@@ -88,8 +88,20 @@ def _check_kernel_stubs(so: Path) -> None:
 _FILE_FLAGS: dict[str, list[str]] = {}
 
 
+def _env_file_flags() -> dict[str, list[str]]:
+    """Build-variant A/B: ``SCALING_AMD_FILE_FLAGS="flash_fwd.hip,flash_bwd.hip:-fno-slp-vectorize;gemm.hip:-DX=1"``
+    adds flags to the named sources (with ``SCALING_AMD_BUILD_OUT`` naming the variant's .so, loaded on the GPU box
+    through ``SCALING_AMD_EXT_SO``, ``ops/_ext.py``)."""
+    out: dict[str, list[str]] = {}
+    for part in filter(None, os.environ.get("SCALING_AMD_FILE_FLAGS", "").split(";")):
+        names, _, fl = part.partition(":")
+        for n in names.split(","):
+            out.setdefault(n.strip(), []).extend(fl.split())
+    return out
+
+
 def _compile(src: Path, flags: list[str]) -> Path:
-    flags = flags + _FILE_FLAGS.get(src.name, [])
+    flags = flags + _FILE_FLAGS.get(src.name, []) + _env_file_flags().get(src.name, [])
     obj = _obj_for(src, flags)
     if obj.exists():
         return obj
@@ -107,6 +119,9 @@ def _compile(src: Path, flags: list[str]) -> Path:
 
 
 def ext_path() -> Path:
+    out = os.environ.get("SCALING_AMD_BUILD_OUT")
+    if out:
+        return Path(out).resolve()
     return ROOT / "scaling_amd" / (EXT_NAME + sysconfig.get_config_var("EXT_SUFFIX"))
 
 

@@ -6,6 +6,9 @@ reference implementations that live next to each op.
 """
 from __future__ import annotations
 
+import importlib.util
+import os
+import sys
 from types import ModuleType
 from typing import Optional
 
@@ -17,6 +20,16 @@ _EXT: Optional[ModuleType] = None
 def ext() -> ModuleType:
     global _EXT
     if _EXT is None:
+        variant = os.environ.get("SCALING_AMD_EXT_SO")
+        if variant:  # a build variant for an A/B (scaling_amd/_build.py: SCALING_AMD_FILE_FLAGS / _BUILD_OUT)
+            spec = importlib.util.spec_from_file_location("scaling_amd._C", variant)
+            if spec is None or spec.loader is None:
+                raise RuntimeError(f"SCALING_AMD_EXT_SO={variant}: not a loadable extension")
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["scaling_amd._C"] = mod
+            _EXT = mod
+            return mod
         try:
             from scaling_amd import _C  # type: ignore[attr-defined]
         except ImportError as e:  # pragma: no cover - depends on build state

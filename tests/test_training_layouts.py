@@ -228,7 +228,7 @@ def test_backward_compatibility_with_legacy_checkpoint(device):
     checks = {
         "hidden_states_embedding": emb.activations, "hidden_states_input_layernorm": ln_in,
         "hidden_states_attention": attn, "hidden_states_post_attention_layernorm": ln_post,
-        "hidden_states_mlp": mlp, "hidden_states_layer0": out1.activations, "hidden_states_norm": norm.activations,
+        "hidden_states_mlp": mlp, "hidden_states_layer0": out1.hidden(), "hidden_states_norm": norm.activations,
         "output_logits": logits.activations,
     }
     diffs = {k: (gt[k].float() - v.float().cpu()).abs().max().item() for k, v in checks.items()}
