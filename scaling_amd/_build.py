@@ -84,8 +84,11 @@ def _check_kernel_stubs(so: Path) -> None:
         raise RuntimeError("kernel host stubs missing from the extension:\n" + "\n".join(missing))
 
 
-# per-file device flags (source file name -> extra hipcc flags); none needed at present
-_FILE_FLAGS: dict[str, list[str]] = {}
+# per-file device flags (source file name -> extra hipcc flags).  flash_fwd.hip without SLP vectorisation: hipcc
+# otherwise packs pairs of the softmax's f32 adds / muls into v_pk_*_f32, which beside MFMAs cost more issue cycles
+# than the two scalar instructions they replace (MI355X_MICROARCH.md, "price of one filler"); forward 879-887 ->
+# 897-903 TF at the 7B shape, interleaved A/B, profiles/attn_slp_ab_r5.log.  The backward kernels measured neutral.
+_FILE_FLAGS: dict[str, list[str]] = {"flash_fwd.hip": ["-fno-slp-vectorize"]}
 
 
 def _env_file_flags() -> dict[str, list[str]]:

@@ -51,10 +51,12 @@ def main() -> None:
         res = fn()
         if isinstance(res, list):
             res = out[:, i]
-        err = (res.float() - ref).abs().max().item() / ref.abs().max().item()
+        err = None
+        if "reference" not in name:
+            err = round((res.float() - ref).abs().max().item() / ref.abs().max().item(), 5)
         print(json.dumps({"variant": name, "us": round(s.elapsed_time(e) / 20 * 1000, 1),
                           "tflops": round(2 * size * R * K * N / (s.elapsed_time(e) / 20 / 1000) / 1e12, 1),
-                          "rel_err": round(err, 5), "kernels": kernels}), flush=True)
+                          "rel_err": err, "kernels": kernels}), flush=True)
 
 
 if __name__ == "__main__":

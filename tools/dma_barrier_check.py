@@ -16,7 +16,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FILES = {"flash_fwd.hip": ("fa_fwd_v2_kernel",), "flash_bwd.hip": ("fa_bwd_dkdv_kernel", "fa_bwd_dq_kernel")}
-FLAGS: dict = {}
+sys.path.insert(0, ROOT)
+from scaling_amd._build import _FILE_FLAGS as FLAGS  # noqa: E402  (the extension build's per-file flags)
 
 
 def check_file(name: str, kernels: tuple[str, ...]) -> list[str]:

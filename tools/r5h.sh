@@ -8,5 +8,5 @@ $T 300 python -u tools/attn_repro.py --trials 10 > gpurun_out/r5h_attn_repro.log
 $T 120 python -u tools/bmm_stride_probe.py > gpurun_out/r5h_bmm.log 2>&1
 SCALING_AMD_SINGLE_STREAM=0 RACE_TRACE_RUNS=3 $T 400 python -u tools/race_trace.py --gpus 2 > gpurun_out/r5h_trace_multi.log 2>&1
 RACE_TRACE_RUNS=3 $T 400 python -u tools/race_trace.py --gpus 2 > gpurun_out/r5h_trace_single.log 2>&1
-bash tools/r5d.sh
-bash tools/r5e.sh
+
+
