@@ -79,7 +79,12 @@ def _chunked_forward(x2: torch.Tensor, weight: torch.Tensor, reduce_scatter: boo
         out = torch.empty((T, N), dtype=x2.dtype, device=x2.device)
     for i in range(chunks):
         if reduce_scatter:
-            part = torch.matmul(x4[:, i], wT)  # [size, R, N]: rank r's rows of this piece, rank-major
+            # [size, R, N]: rank r's rows of this piece, rank-major, as one contiguous-operand GEMM per rank block.
+            # (torch.matmul on the strided [size, R, K] view x4[:, i] -- batch stride chunks*R*K -- faulted on
+            # MI355X with an illegal memory access inside the vendor GEMM, profiles/matmul_strided_fault_r5.log)
+            part = torch.empty((size, R, N), dtype=x2.dtype, device=x2.device)
+            for r in range(size):
+                torch.mm(x4[r, i], wT, out=part[r])
             dst = out[i * R : (i + 1) * R]
         else:
             part = out[i * R : (i + 1) * R]

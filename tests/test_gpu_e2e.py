@@ -267,3 +267,18 @@ def test_gpu_nt_gemm_training_matches_vendor_path(extra):
     assert np.isfinite(nt["loss"]) and np.isfinite(ref["loss"])
     assert abs(nt["loss"] - ref["loss"]) < 2e-2 * abs(ref["loss"]), (nt["loss"], ref["loss"])
     assert all(np.isfinite(v) for v in nt["param_checksum"])
+
+
+def test_gpu_shard_proxy_tp_chunks_match():
+    """BASELINE #3's per-rank shard (TP2 + sequence parallelism, collectives stubbed) with the row-parallel GEMMs cut
+    into 1 / 2 / 4 overlapped token pieces and the norm gathers folded into their GEMMs trains to the same losses: the
+    chunked sequence-parallel forward runs one contiguous-operand GEMM per rank block of each piece (a strided
+    batched matmul over the pieces faulted, profiles/matmul_strided_fault_r5.log)."""
+    losses = {}
+    for c in ("1", "2", "4"):
+        cfg = _bench_loss({}, ["--shard-proxy", "baseline3", "--tp-comm-chunks", c, "--micro-batch", "8"])
+        assert cfg["shard_proxy"] == "baseline3" and cfg["tp"] == 2 and cfg["sequence_parallel"]
+        losses[c] = cfg["loss"]
+        assert np.isfinite(cfg["loss"]) and all(np.isfinite(v) for v in cfg["param_checksum"])
+    assert abs(losses["2"] - losses["1"]) < 1e-3 * abs(losses["1"]), losses
+    assert abs(losses["4"] - losses["1"]) < 1e-3 * abs(losses["1"]), losses
