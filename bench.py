@@ -354,7 +354,11 @@ def _worker(a: argparse.Namespace) -> None:
         raise SystemExit(3)
     model = init_model(context=context)
     optimizer = init_optimizer(context=context, model=model)
-    loader = _SyntheticLoader(a.micro_batch, a.seq_len, arch["vocab_size"], seed=1234 + topology.data_parallel_rank,
+    # per-rank proxy: token ids from rank 0's vocabulary shard.  The stubbed collectives cannot sum the other shard's
+    # embedding rows in, so an id outside the shard would embed as a zero vector (in the real layout the TP all-reduce
+    # supplies it); such rows normalise to ~0 and their gradient explodes through every norm of the backward
+    vocab = arch["vocab_size"] // a.tp if a.shard_proxy else arch["vocab_size"]
+    loader = _SyntheticLoader(a.micro_batch, a.seq_len, vocab, seed=1234 + topology.data_parallel_rank,
                               pin=gpu)
 
     def sync() -> None:
@@ -397,6 +401,41 @@ def _worker(a: argparse.Namespace) -> None:
         from scaling_amd.core.utils import grad_probe
 
         grad_probe.enable(gtrace)  # + the probes inside the layers (attention input / q,k,v / core output, layer input)
+
+    if os.environ.get("SCALING_AMD_BENCH_NORMS") == "1":  # debug: per-module output / per-parameter gradient magnitudes
+        def _norm_hook(name: str) -> Any:
+            def hook(_m: Any, _inp: Any, out: Any) -> None:
+                t = out if torch.is_tensor(out) else getattr(out, "activations", None)
+                if torch.is_tensor(t) and t.is_floating_point() and rank == 0:
+                    f = t.detach().float()
+                    print(f"[norms] fwd {name}: absmax {f.abs().max().item():.4g} rms {f.pow(2).mean().sqrt().item():.4g}",
+                          file=sys.stderr, flush=True)
+                    if t.requires_grad:
+                        t.register_hook(lambda g, n=name: print(
+                            f"[norms] bwd into {n}: absmax {g.detach().float().abs().max().item():.4g}", file=sys.stderr,
+                            flush=True))
+                    br = getattr(out, "residual_branch", None)
+                    if torch.is_tensor(br) and br.requires_grad:
+                        br.register_hook(lambda g, n=name: print(
+                            f"[norms] bwd into {n}.residual_branch: absmax {g.detach().float().abs().max().item():.4g}",
+                            file=sys.stderr, flush=True))
+            return hook
+
+        for mname, mod in model.named_modules():
+            if mname.count(".") <= 3 and mname:
+                mod.register_forward_hook(_norm_hook(mname))
+        orig_step2 = optimizer.step
+
+        def norm_step() -> Any:
+            if rank == 0:
+                for n, p in model.named_parameters():
+                    if p.grad is not None:
+                        g = p.grad.detach().float()
+                        print(f"[norms] grad {n}: absmax {g.abs().max().item():.4g} finite {bool(torch.isfinite(g).all())}",
+                              file=sys.stderr, flush=True)
+            return orig_step2()
+
+        optimizer.step = norm_step
 
     def step() -> Any:
         out = model.train_step(loader, optimizer, TextDataset.sync_batch_to_model_parallel, loss_function,

@@ -145,6 +145,9 @@ def _sp_backward_chunked(ctx: Any, g: torch.Tensor) -> tuple:
     cs = _tp_comm_stream(g.device)
     main = torch.cuda.current_stream(g.device) if cs is not None else None
     pieces, events = [], []
+    # the full-token (rank-major) gradient for the weight-gradient GEMM: each piece is copied into place on the
+    # communication stream right behind its all-gather, so the copies run beside the input-gradient GEMMs
+    gfull = torch.empty((size, chunks, R, N), dtype=g.dtype, device=g.device)
     for i in range(chunks):
         buf = torch.empty((size, R, N), dtype=g.dtype, device=g.device)
         if cs is not None:
@@ -154,18 +157,18 @@ def _sp_backward_chunked(ctx: Any, g: torch.Tensor) -> tuple:
                 dist.all_gather_into_tensor(buf.view(-1), gl[i].reshape(-1), group=group)
                 ev = torch.cuda.Event()
                 ev.record(cs)
+                gfull[:, i].copy_(buf)
             events.append(ev)
         else:
             dist.all_gather_into_tensor(buf.view(-1), gl[i].reshape(-1), group=group)
+            gfull[:, i].copy_(buf)
         pieces.append(buf)
-    gfull = torch.empty((size, chunks, R, N), dtype=g.dtype, device=g.device)  # full-token (rank-major) order
     dx = torch.empty((size, chunks, R, K), dtype=g.dtype, device=g.device) if ctx.needs_input_grad[0] else None
     wmat = w.t() if ctx.has_wt else w  # [N, K]
     for i in range(chunks):
         if cs is not None:
             assert main is not None
             main.wait_event(events[i])
-        gfull[:, i].copy_(pieces[i])
         if dx is not None:
             for r in range(size):
                 torch.mm(pieces[i][r], wmat, out=dx[r, i])

@@ -30,3 +30,24 @@ def probe(name: str, t: Any) -> Any:
         t.register_hook(lambda g, n=name: rec.append(
             (n, torch.stack([g.double().sum(), (g.double() * g.double()).sum()]))))
     return t
+
+
+def record(name: str, *tensors: Any) -> None:
+    """Appends ``(name, [sum, sum of squares] per tensor)`` of arbitrary tensors (saved activations, buffers) at this
+    point of the stream, when probing is on: e.g. an op's saved inputs once in its forward and again at the start of
+    its backward, so a change in between (something writing into memory it does not own) shows up as a differing
+    entry."""
+    rec = _records
+    if rec is None:
+        return
+    vals = []
+    for t in tensors:
+        if torch.is_tensor(t) and t.numel():
+            d = t.detach().double()
+            vals += [d.sum(), (d * d).sum()]
+    if vals:
+        rec.append((name, torch.stack(vals)))
+
+
+def enabled() -> bool:
+    return _records is not None

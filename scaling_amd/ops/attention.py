@@ -218,6 +218,13 @@ def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
     return base.as_strided(shape, stride, base.storage_offset() + off)
 
 
+def _probe_record(name: str, *tensors: Any) -> None:
+    """Race-check forensics (``core/utils/grad_probe.record``; a no-op unless probing is on)."""
+    from ..core.utils import grad_probe  # deferred: scaling_amd.core imports this module
+
+    grad_probe.record(name, *tensors)
+
+
 class _RopeFlashAttn(torch.autograd.Function):
     """RoPE on q/k + flash attention over views of ONE projection output (``base``).
 
@@ -234,12 +241,15 @@ class _RopeFlashAttn(torch.autograd.Function):
         k = ext().rope(ki, cos, sin, pos, rot_dim, seq_len, interleaved, False)
         o, lse = _fa_fwd_stashed(q, k, vi, cu_q, cu_k, max_q, scale, causal, window, p_drop, seed, local_heads, max_k)
         ctx.save_for_backward(base, q, k, o, lse, cu_q, cu_k, cos, sin, pos)
+        _probe_record("rope_flash.saved@fwd", base, q, k, o, lse, pos, cos, sin, cu_q)
         ctx.cfg = (specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads)
         return o
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
+        _probe_record("rope_flash.saved@bwd", base, q, k, o, lse, pos, cos, sin, cu_q)
+        _probe_record("rope_flash.do", do)
         specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)

@@ -50,7 +50,7 @@ def main() -> None:
         return
     import torch
 
-    from scaling_amd.ops import attention
+    from scaling_amd.ops import attention, rope
 
     dev = torch.device("cuda")
     side = torch.cuda.Stream()
@@ -65,11 +65,29 @@ def main() -> None:
         do = torch.randn(T, HQ, D, device=dev, dtype=torch.bfloat16, generator=g)
         sc = 1 / math.sqrt(D)
 
-        def run():
+        cos, sin = rope.rope_tables(D, S, 10000, False, torch.bfloat16, dev)
+        pos = torch.arange(S, device=dev).repeat(ns)
+        base0 = torch.cat([q0.reshape(T, -1), k0.reshape(T, -1), v0.reshape(T, -1)], dim=1)
+
+        def run_plain():
             q, k, v = (t.clone().requires_grad_(True) for t in (q0, k0, v0))
             o = attention.flash_attention(q, k, v, cu, cu, S, S, sc, True, None)
             o.backward(do)
             return [o.detach(), q.grad, k.grad, v.grad]
+
+        def run_rope():  # the training path: RoPE fused into the attention (inverse rotation in the dQ/dK epilogues)
+            base = base0.clone().requires_grad_(True)
+            nq, nk = HQ * D, HK * D
+            q = base[:, :nq].view(T, HQ, D)
+            k = base[:, nq:nq + nk].view(T, HK, D)
+            v = base[:, nq + nk:].view(T, HK, D)
+            o = attention.rope_flash_attention(base, q, k, v, cos, sin, pos, D, S, False, cu, S, sc, True)
+            assert o is not None, "fused rope + flash path declined"
+            o.backward(do)
+            g = base.grad
+            return [o.detach(), g[:, :nq], g[:, nq:nq + nk], g[:, nq + nk:]]
+
+        run = run_rope if os.environ.get("ATTN_REPRO_ROPE", "1") == "1" else run_plain
 
         torch.cuda.synchronize()
         ref = run()

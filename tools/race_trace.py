@@ -59,6 +59,9 @@ def main():
                     if key == "gtrace" and x[key] != y[key]:
                         idx = [j for j, (u, v) in enumerate(zip(x[key], y[key])) if u != v]
                         j0 = idx[0]
+                        names = [x[key][j][0] for j in idx[:12]]
+                        print(f"   step {x['step']}: {len(idx)} of {len(x[key])} trace entries differ, first: {names}",
+                              flush=True)
                         first = (x["step"], f"gtrace: first differing input gradient #{j0} of {len(x[key])} "
                                  f"(backward order) entering {x[key][j0][0]}: {x[key][j0][1]} vs {y[key][j0][1]}; "
                                  f"previous entries: {[e[0] for e in x[key][max(0, j0 - 3):j0]]}",
