@@ -53,7 +53,9 @@ def _broadcast(tensor: torch.Tensor, src: Any = None, group: Any = None, async_o
 
 def _all_gather_into_tensor(output: torch.Tensor, input: torch.Tensor, group: Any = None, async_op: bool = False) -> Any:
     n = dist.get_world_size(group)
-    output.view(n, -1).copy_(input.reshape(1, -1).expand(n, -1))
+    flat, src = output.view(n, -1), input.reshape(-1)
+    for i in range(n):  # contiguous device copies (a broadcast copy_ runs a slow strided elementwise kernel)
+        flat[i].copy_(src)
     return _ret(async_op)
 
 
