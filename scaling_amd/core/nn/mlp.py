@@ -10,7 +10,8 @@ GEMM-keeping activation-checkpoint region) the whole MLP is ONE autograd node on
 down-projection input gradient consumes ``dh`` in registers and writes ``dz`` directly -- no SwiGLU pass over HBM in
 either direction.
 
-Otherwise, where ``ops.gemm.nt_swiglu_bwd_enabled`` picks the shape (the 7B one by default), only the backward is fused:
+Otherwise, where ``ops.gemm.nt_swiglu_bwd_enabled`` picks the shape (opt-in; measured slower in the 7B step), only the
+backward is fused:
 ``_SwiGLUDown`` runs the unfused forward (SwiGLU kernel + hipBLASLt down projection) and computes ``dz`` from the down
 projection's input-gradient GEMM with the SwiGLU backward in its epilogue (no dh round trip through HBM, no stand-alone
 SwiGLU backward pass).

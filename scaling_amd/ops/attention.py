@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 import threading
 from typing import Callable, Any, Iterator, Optional
 
@@ -218,6 +219,9 @@ def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
     return base.as_strided(shape, stride, base.storage_offset() + off)
 
 
+_DEBUG_SYNC_FA = os.environ.get("SCALING_AMD_DEBUG_SYNC_FA") == "1"
+
+
 def _probe_record(name: str, *tensors: Any) -> None:
     """Race-check forensics (``core/utils/grad_probe.record``; a no-op unless probing is on)."""
     from ..core.utils import grad_probe  # deferred: scaling_amd.core imports this module
@@ -255,8 +259,14 @@ class _RopeFlashAttn(torch.autograd.Function):
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
         v = _view(base, specs[2])
         # the inverse rotation of dq / dk is folded into the attention backward's dQ / dK epilogues
+        sync = _DEBUG_SYNC_FA and base.is_cuda
+        if sync:  # race forensics: nothing else may run beside the attention backward
+            torch.cuda.synchronize(base.device)
         ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
                      local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+        if sync:
+            torch.cuda.synchronize(base.device)
+        _probe_record("rope_flash.dbase", dbase)
         return (dbase,) + (None,) * 17
 
 

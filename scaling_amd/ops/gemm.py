@@ -78,10 +78,12 @@ def nt_fused_mlp_enabled(a: torch.Tensor, wgu: torch.Tensor) -> bool:
 
 
 # (F, H) down-projection shapes where the backward's dh = dY W_down GEMM with the SwiGLU backward in its epilogue
-# (``gemm_nt_swiglu_bwd``: writes dz, no dh round trip, no stand-alone SwiGLU backward pass) beat hipBLASLt + the
-# SwiGLU backward kernel: 2.576 vs 2.606 ms per 7B layer (profiles/gemm_nt_swiglu_bwd_pipelined_r4.log).  Used with
-# the unfused forward (hipBLASLt gate/up GEMM + SwiGLU kernel), which is faster than the fused one at this shape.
-NT_SWIGLU_BWD: set[tuple[int, int]] = {(11008, 4096)}
+# (``gemm_nt_swiglu_bwd``: writes dz, no dh round trip, no stand-alone SwiGLU backward pass; used with the unfused
+# forward) beats hipBLASLt + the SwiGLU backward kernel.  Empty: isolated, the 7B shape (11008, 4096) measured 2.576 vs
+# 2.606 ms per layer (profiles/gemm_nt_swiglu_bwd_pipelined_r4.log), but inside the training step the NT kernel takes
+# 84.7 ms per step against ~72 ms for what it replaces and the step is 1-2 ms slower (interleaved A/B,
+# profiles/swiglu_bwd_nt_ab_r5.log).  SCALING_AMD_SWIGLU_BWD_NT=1 turns it on for every shape the kernel tiles.
+NT_SWIGLU_BWD: set[tuple[int, int]] = set()
 _SWIGLU_BWD_MODE = os.environ.get("SCALING_AMD_SWIGLU_BWD_NT", "auto")
 
 
