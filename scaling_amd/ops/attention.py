@@ -220,6 +220,7 @@ def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
 
 
 _DEBUG_SYNC_FA = os.environ.get("SCALING_AMD_DEBUG_SYNC_FA") == "1"
+_DEBUG_FA_TWICE = os.environ.get("SCALING_AMD_DEBUG_FA_TWICE") == "1"
 
 
 def _probe_record(name: str, *tensors: Any) -> None:
@@ -267,6 +268,12 @@ class _RopeFlashAttn(torch.autograd.Function):
         if sync:
             torch.cuda.synchronize(base.device)
         _probe_record("rope_flash.dbase", dbase)
+        if _DEBUG_FA_TWICE:  # race forensics: the same backward again, into a second buffer; record any difference
+            d2 = torch.empty_like(base)
+            q2, k2, v2 = (_view(d2, sp) for sp in specs)
+            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q2, k2, v2, p_drop, seed,
+                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+            _probe_record("rope_flash.twice_mismatch", (d2 != dbase).sum().double().reshape(1))
         return (dbase,) + (None,) * 17
 
 
