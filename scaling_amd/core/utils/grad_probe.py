@@ -51,3 +51,10 @@ def record(name: str, *tensors: Any) -> None:
 
 def enabled() -> bool:
     return _records is not None
+
+
+def record_values(name: str, t: Any) -> None:
+    """Appends ``(name, t)`` itself (a small float64 vector of diagnostic values) when probing is on."""
+    rec = _records
+    if rec is not None and torch.is_tensor(t):
+        rec.append((name, t.detach().double().reshape(-1)))

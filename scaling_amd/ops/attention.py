@@ -220,6 +220,12 @@ def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
 
 
 _DEBUG_SYNC_FA = os.environ.get("SCALING_AMD_DEBUG_SYNC_FA") == "1"
+
+
+def _probe_values(name: str, t: torch.Tensor) -> None:
+    from ..core.utils import grad_probe  # deferred: scaling_amd.core imports this module
+
+    grad_probe.record_values(name, t)
 _DEBUG_FA_TWICE = os.environ.get("SCALING_AMD_DEBUG_FA_TWICE") == "1"
 
 
@@ -273,7 +279,13 @@ class _RopeFlashAttn(torch.autograd.Function):
             q2, k2, v2 = (_view(d2, sp) for sp in specs)
             ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q2, k2, v2, p_drop, seed,
                          local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
-            _probe_record("rope_flash.twice_mismatch", (d2 != dbase).sum().double().reshape(1))
+            ne = d2 != dbase
+            first = torch.nonzero(ne.reshape(-1))[:4].reshape(-1).double()
+            counts = torch.stack([(a != b).sum() for a, b in zip((q2, k2, v2), (dq, dk, dv))]).double()
+            _probe_values("rope_flash.twice_mismatch", torch.cat([ne.sum().double().reshape(1), counts,
+                                                                   first, torch.tensor([float(dbase.shape[-1])],
+                                                                                       device=first.device,
+                                                                                       dtype=torch.float64)]))
         return (dbase,) + (None,) * 17
 
 

@@ -29,11 +29,12 @@ from ._ext import ext, use_native
 
 
 _WGRAD_RAGGED = os.environ.get("SCALING_AMD_WGRAD_RAGGED", "1") != "0"
+_WGRAD_HIP = os.environ.get("SCALING_AMD_WGRAD_HIP", "1") != "0"  # 0: every weight gradient on hipBLASLt (A/B, forensics)
 
 
 def wgrad(dy: torch.Tensor, x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
     """``out (+)= dy^T @ x`` for 2-D ``dy [T, N]``, ``x [T, K]``; returns ``out`` ([N, K])."""
-    if use_native(dy):
+    if use_native(dy) and _WGRAD_HIP:
         o = out if out is not None else torch.empty(dy.shape[1], x.shape[1], device=dy.device, dtype=dy.dtype)
         ragged = dy.shape[1] % 256 != 0 or x.shape[1] % 256 != 0
         if (_WGRAD_RAGGED or not ragged) and ext().gemm_tn_ok(dy, x, o):
