@@ -8,6 +8,7 @@ reference computed on an idle GPU and counts mismatching iterations while a seco
     hip_wgrad   this framework's weight-gradient GEMM (gemm_tn_ring_kernel: LDS-DMA ring, transposing LDS reads)
     blas        a hipBLASLt GEMM (torch.matmul)
     attn        this framework's attention forward + backward
+    bench       a whole llama_tiny training run (bench.py, one process)
 
     python tools/attn_stress.py --iters 2000 --hammer hip_wgrad
 """
@@ -17,6 +18,7 @@ import argparse
 import json
 import math
 import os
+import signal
 import subprocess
 import sys
 import time
@@ -27,6 +29,22 @@ SHAPES = {"race_tiny": (2, 256, 4, 2, 64), "d128": (2, 1024, 16, 4, 128)}
 
 
 def hammer(kind: str, seconds: float) -> None:
+    if kind == "bench":  # the full llama_tiny training step mix (norms, SwiGLU, GEMMs, attention, AdamW, copies)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
+        q = subprocess.Popen([sys.executable, os.path.join(root, "bench.py"), "--model", "llama_tiny", "--seq-len", "256",
+                              "--micro-batch", "2", "--steps", "100000", "--warmup", "1"], cwd=root, env=env,
+                             stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        time.sleep(20)  # model build + first steps
+        print("ready", flush=True)
+        try:
+            q.wait(timeout=seconds)
+        except subprocess.TimeoutExpired:
+            pass
+        finally:
+            q.kill()
+            q.wait()
+        return
     import torch
 
     from scaling_amd.ops import gemm
@@ -86,21 +104,23 @@ def _attn_case(torch, name):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=2000)
-    ap.add_argument("--hammer", default="none", choices=["none", "hip_wgrad", "blas", "attn"])
+    ap.add_argument("--hammer", default="none", choices=["none", "hip_wgrad", "blas", "attn", "bench"])
     ap.add_argument("--shape", default="race_tiny", choices=sorted(SHAPES))
     ap.add_argument("--child", type=float, default=0.0)
     a = ap.parse_args()
     if a.child:
         hammer(a.hammer, a.child)
         return
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(1))  # a time limit still runs the finally below
     import torch
 
     run, (HQ, HK, D, T) = _attn_case(torch, a.shape)
     torch.cuda.synchronize()
     ref_o, ref_g = run()
     torch.cuda.synchronize()
+    # own process group: the hammer and anything it starts (the bench hammer's training process) end together
     p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--hammer", a.hammer, "--child", "240"],
-                         stdout=subprocess.PIPE, text=True)
+                         stdout=subprocess.PIPE, text=True, start_new_session=True)
     bad, bad_o, where = 0, 0, {}
     try:
         assert p.stdout is not None and p.stdout.readline().strip() == "ready"
@@ -121,7 +141,7 @@ def main() -> None:
             if time.time() - t0 > 200:
                 break
     finally:
-        p.kill()
+        os.killpg(p.pid, signal.SIGKILL)
         p.wait()
     print(json.dumps({"shape": a.shape, "hammer": a.hammer, "iters": it + 1, "mismatch_grad": bad, "mismatch_out": bad_o,
                       "regions": where}), flush=True)

@@ -24,7 +24,7 @@ for step in "$@"; do
     echo "[gpu.sh] $step $(date +%T)"
     case "$step" in
     tests)
-        $T 900 $PY -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
+        $T 1000 $PY -m pytest tests -m gpu -v --durations=40 --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
             > gpurun_out/tests_$TAG.log 2>&1 ;;
     smoke)
         $T 180 $PY -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 ;;
