@@ -39,7 +39,11 @@ SMALL = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "
 )
 def test_bench_rehearsal_gloo_gpu(layout):
     gpus, tp, pp, acc, extra = layout
-    r = _run(["--gpus", gpus, "--tp", tp, "--pp", pp, "--grad-acc", acc, *SMALL, *extra], timeout=300)
+    if "--preset" in extra:  # the preset owns the layout flags (an explicit conflicting one is an error)
+        small = [a for i, a in enumerate(SMALL) if a != "--micro-batch" and SMALL[i - 1] != "--micro-batch"]
+        r = _run(["--gpus", gpus, *small, *extra], timeout=300)
+    else:
+        r = _run(["--gpus", gpus, "--tp", tp, "--pp", pp, "--grad-acc", acc, *SMALL, *extra], timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
@@ -264,7 +268,7 @@ def test_keep_attention_checkpointing_gpu(tmp_path):
         try:
             out = checkpoint_with_rng(layer._forward_tuple_input, None, True, *layer.input_to_tuple(io),
                                       keep_attention=keep)
-            out.activations.float().pow(2).mean().backward()
+            out.hidden().float().pow(2).mean().backward()
             torch.cuda.synchronize()
         finally:
             e.fa_fwd = real

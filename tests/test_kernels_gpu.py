@@ -125,7 +125,7 @@ def test_norm_passthrough_and_layer_fusion():
     cu = torch.arange(0, (seqs + 1) * T, T, device=DEV, dtype=torch.int32)
     pos = torch.arange(T, device=DEV).repeat(seqs, 1)
     out = layer(TransformerLayerIO(activations=a, position_ids=pos, cumulative_seq_lengths_padded=cu,
-                                   cumulative_seq_lengths=cu)).activations
+                                   cumulative_seq_lengths=cu)).hidden()
     g = torch.randn_like(out)
     out.backward(g)
     ga, gw = a.grad.clone(), [p.grad.clone() for p in layer.parameters()]

@@ -234,7 +234,7 @@ def test_save_matmuls_checkpointing_skips_gemms_in_recompute():
             out = checkpoint_with_rng(layer._forward_tuple_input, None, True, *layer.input_to_tuple(io),
                                       keep_gemms=gemms)
             n_fwd = len(calls)
-            out.activations.pow(2).mean().backward()
+            out.hidden().pow(2).mean().backward()
         finally:
             mg.gemm_linear = real
         assert n_fwd > 0
