@@ -187,6 +187,10 @@ def _launch(a: argparse.Namespace) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if a.backend == "gloo":  # CPU ranks: do not oversubscribe the host's cores
             env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // a.gpus)))
+        cus = int(os.environ.get("SCALING_AMD_REHEARSAL_CU_SPLIT", "0") or 0)
+        if a.backend == "gloo-gpu" and cus:  # rehearsal ranks sharing one GPU: each on its own CUs, as on its own GPU
+            per = cus // a.gpus
+            env["HSA_CU_MASK"] = f"0:{r * per}-{(r + 1) * per - 1}"
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
 
     def _kill_all(sig: int) -> None:
