@@ -279,13 +279,27 @@ class _RopeFlashAttn(torch.autograd.Function):
             q2, k2, v2 = (_view(d2, sp) for sp in specs)
             ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q2, k2, v2, p_drop, seed,
                          local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+            d3 = torch.empty_like(base)  # a third time: which of the two is the odd one out
+            q3, k3, v3 = (_view(d3, sp) for sp in specs)
+            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q3, k3, v3, p_drop, seed,
+                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
             ne = d2 != dbase
-            first = torch.nonzero(ne.reshape(-1))[:4].reshape(-1).double()
+            f64 = dict(device=base.device, dtype=torch.float64)
+            first = torch.full((4,), -1.0, **f64)
+            nz = torch.nonzero(ne.reshape(-1))[:4].reshape(-1).double()
+            first[:nz.numel()] = nz
             counts = torch.stack([(a != b).sum() for a, b in zip((q2, k2, v2), (dq, dk, dv))]).double()
-            _probe_values("rope_flash.twice_mismatch", torch.cat([ne.sum().double().reshape(1), counts,
-                                                                   first, torch.tensor([float(dbase.shape[-1])],
-                                                                                       device=first.device,
-                                                                                       dtype=torch.float64)]))
+            # [total, dq, dk, dv, first 4 flat indices, row length, d3 == first, d3 == second, distinct rows,
+            #  max |difference|, up to 16 distinct columns (-1 padded)]
+            rows_ne, cols_ne = ne.reshape(ne.shape[0], -1).any(1), ne.reshape(ne.shape[0], -1).any(0)
+            cols = torch.full((16,), -1.0, **f64)
+            cz = torch.nonzero(cols_ne).reshape(-1)[:16].double()
+            cols[:cz.numel()] = cz
+            extra = torch.stack([torch.equal(d3, dbase) * torch.ones((), **f64), torch.equal(d3, d2) * torch.ones((), **f64),
+                                 rows_ne.sum().double(), (d2.float() - dbase.float()).abs().max().double()])
+            _probe_values("rope_flash.twice_mismatch", torch.cat([ne.sum().double().reshape(1), counts, first,
+                                                                   torch.tensor([float(dbase.shape[-1])], **f64), extra,
+                                                                   cols]))
         return (dbase,) + (None,) * 17
 
 
