@@ -227,6 +227,7 @@ def _probe_values(name: str, t: torch.Tensor) -> None:
 
     grad_probe.record_values(name, t)
 _DEBUG_FA_TWICE = os.environ.get("SCALING_AMD_DEBUG_FA_TWICE") == "1"
+_DEBUG_UNFOLD_ROPE = os.environ.get("SCALING_AMD_DEBUG_UNFOLD_ROPE") == "1"
 
 
 def _probe_record(name: str, *tensors: Any) -> None:
@@ -267,22 +268,30 @@ class _RopeFlashAttn(torch.autograd.Function):
         v = _view(base, specs[2])
         # the inverse rotation of dq / dk is folded into the attention backward's dQ / dK epilogues
         sync = _DEBUG_SYNC_FA and base.is_cuda
+
+        def bwd_into(gq, gk, gv):
+            if _DEBUG_UNFOLD_ROPE:  # race forensics: plain dQ / dK epilogues, then the stand-alone inverse RoPE
+                ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, gq, gk, gv, p_drop,
+                             seed, local_heads)
+                gq.copy_(ext().rope(gq.contiguous(), cos, sin, pos, rot_dim, seq_len, interleaved, True))
+                gk.copy_(ext().rope(gk.contiguous(), cos, sin, pos, rot_dim, seq_len, interleaved, True))
+                return
+            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, gq, gk, gv, p_drop, seed,
+                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+
         if sync:  # race forensics: nothing else may run beside the attention backward
             torch.cuda.synchronize(base.device)
-        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
-                     local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+        bwd_into(dq, dk, dv)
         if sync:
             torch.cuda.synchronize(base.device)
         _probe_record("rope_flash.dbase", dbase)
         if _DEBUG_FA_TWICE:  # race forensics: the same backward again, into a second buffer; record any difference
             d2 = torch.empty_like(base)
             q2, k2, v2 = (_view(d2, sp) for sp in specs)
-            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q2, k2, v2, p_drop, seed,
-                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+            bwd_into(q2, k2, v2)
             d3 = torch.empty_like(base)  # a third time: which of the two is the odd one out
             q3, k3, v3 = (_view(d3, sp) for sp in specs)
-            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, q3, k3, v3, p_drop, seed,
-                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+            bwd_into(q3, k3, v3)
             ne = d2 != dbase
             f64 = dict(device=base.device, dtype=torch.float64)
             first = torch.full((4,), -1.0, **f64)
@@ -297,9 +306,14 @@ class _RopeFlashAttn(torch.autograd.Function):
             cols[:cz.numel()] = cz
             extra = torch.stack([torch.equal(d3, dbase) * torch.ones((), **f64), torch.equal(d3, d2) * torch.ones((), **f64),
                                  rows_ne.sum().double(), (d2.float() - dbase.float()).abs().max().double()])
+            vals = torch.zeros(8, **f64)  # the first 4 differing elements: first run, then second run
+            ix = first[:nz.numel()].long()
+            vals[:nz.numel()] = dbase.reshape(-1)[ix].double()
+            vals[4:4 + nz.numel()] = d2.reshape(-1)[ix].double()
+            # [..., 16 columns, 8 values]
             _probe_values("rope_flash.twice_mismatch", torch.cat([ne.sum().double().reshape(1), counts, first,
                                                                    torch.tensor([float(dbase.shape[-1])], **f64), extra,
-                                                                   cols]))
+                                                                   cols, vals]))
         return (dbase,) + (None,) * 17
 
 
