@@ -187,8 +187,12 @@ def _launch(a: argparse.Namespace) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if a.backend == "gloo":  # CPU ranks: do not oversubscribe the host's cores
             env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // a.gpus)))
-        cus = int(os.environ.get("SCALING_AMD_REHEARSAL_CU_SPLIT", "0") or 0)
-        if a.backend == "gloo-gpu" and cus:  # rehearsal ranks sharing one GPU: each on its own CUs, as on its own GPU
+        # rehearsal ranks sharing one GPU: each on a disjoint CU range, as it would own a GPU (value: the device's CU
+        # count, "1" = MI355X's 256).  Waves of two ranks co-resident on one CU made ~0.2-1 % of attention backwards
+        # differ by <= 1 bf16 ulp from a recomputation in place; 0 of 768 with the split (profiles/race_forensics_r5.md)
+        split = os.environ.get("SCALING_AMD_REHEARSAL_CU_SPLIT", "0") or "0"
+        cus = 256 if split == "1" else int(split)
+        if a.backend == "gloo-gpu" and cus and a.gpus > 1:
             per = cus // a.gpus
             env["HSA_CU_MASK"] = f"0:{r * per}-{(r + 1) * per - 1}"
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))

@@ -180,3 +180,31 @@ def test_bench_shard_proxy_gloo(preset, ac):
     assert c["activation_checkpointing"] == (ac or ("every_layer_save_matmuls" if preset == "baseline4" else "disabled"))
     assert c["micro_batch"] == (4 if preset == "baseline4" else 8) and math.isfinite(c["loss"])
     assert c["proxy_8gpu_tokens_s_without_comm"] > 0
+
+
+@pytest.mark.parametrize("split,gpus,backend,want", [("1", 2, "gloo-gpu", ["0:0-127", "0:128-255"]),
+                                                     ("256", 4, "gloo-gpu", ["0:0-63", "0:64-127", "0:128-191", "0:192-255"]),
+                                                     ("1", 2, "gloo", [None, None]), ("0", 2, "gloo-gpu", [None, None])])
+def test_bench_launcher_cu_split(monkeypatch, split, gpus, backend, want):
+    """SCALING_AMD_REHEARSAL_CU_SPLIT gives each 1-GPU rehearsal rank a disjoint CU range (HSA_CU_MASK), only for the
+    GPU-sharing gloo-gpu backend."""
+    import argparse
+
+    import bench
+
+    envs = []
+
+    class _Proc:
+        def __init__(self, argv, env):
+            envs.append(env)
+
+        def poll(self):
+            return 0
+
+    monkeypatch.setenv("SCALING_AMD_REHEARSAL_CU_SPLIT", split)
+    monkeypatch.delenv("HSA_CU_MASK", raising=False)
+    monkeypatch.setattr(bench.subprocess, "Popen", _Proc)
+    monkeypatch.setattr(bench.signal, "signal", lambda *a: None)
+    a = argparse.Namespace(gpus=gpus, backend=backend, launch_timeout=10)
+    assert bench._launch(a) == 0
+    assert [e.get("HSA_CU_MASK") for e in envs] == want

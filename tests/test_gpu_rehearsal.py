@@ -126,12 +126,17 @@ def test_race_check_multi_stream_equals_single_stream(args, env):
     every wave's LDS-DMA pieces of the next tile (flash_attn.h: dma_barrier; tools/dma_barrier_check.py).  Both runs use library-side determinism
     (SCALING_AMD_DETERMINISTIC=1: torch deterministic algorithms, rocBLAS without atomics): with several ranks sharing
     the one GPU, the default vendor GEMM kernels' atomic accumulation order varies from run to run even with every
-    stream folded (profiles/race_repeat_dp2_r4.log), which would hide what this test checks."""
+    stream folded (profiles/race_repeat_dp2_r4.log), which would hide what this test checks.  Several ranks run each on
+    a disjoint CU range (SCALING_AMD_REHEARSAL_CU_SPLIT, bench.py), as each would own a GPU: with two ranks' waves
+    co-resident on one CU, ~0.2-1 % of attention backwards came out <= 1 bf16 ulp different from the same backward
+    recomputed in place (a third computation agreeing with the first; no stream of the process involved), 0 of 768 with
+    the split (profiles/race_forensics_r5.md)."""
     base = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
             "--warmup", "1"]
+    split = {"SCALING_AMD_REHEARSAL_CU_SPLIT": "1"} if args[1] != "1" else {}
     out = {}
     for mode, extra in (("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})):
-        r = _run([*base, *args], env_extra={**env, **extra, "SCALING_AMD_DETERMINISTIC": "1"}, timeout=300)
+        r = _run([*base, *args], env_extra={**env, **extra, **split, "SCALING_AMD_DETERMINISTIC": "1"}, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
         res = _json_lines(r.stdout)[0]["config"]
         out[mode] = (res["param_checksum"], res["loss"])
