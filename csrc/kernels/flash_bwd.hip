@@ -14,6 +14,18 @@
 using namespace sa;
 using namespace sa::fa;
 
+// race forensics: pad between the last MFMAs of a kernel and its epilogue's reads of their accumulators
+#ifndef SA_FA_BWD_EPI_PAD
+#define SA_FA_BWD_EPI_PAD 0
+#endif
+__device__ __forceinline__ void epi_pad() {
+    if constexpr (SA_FA_BWD_EPI_PAD) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 template <int D, typename E>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
                                                          const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
@@ -376,6 +388,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         dma_barrier();
     }
     if (w < nwork) tile(buf0, cg, cq);
+    epi_pad();
 
     if (mykey < Lk) {
         if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel
@@ -545,6 +558,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_DQ_ISSUE
+    epi_pad();
     if (myq < Lq)
         store_grad_row<D, F16>(a, dq, a.scale, q0s + myq, h,
                                a.dq + (int64_t)(q0s + myq) * a.dq_tok + (int64_t)hq * a.dq_head);
