@@ -6,6 +6,7 @@ usage: python tools/rocpd_step.py <run_results.db>
 """
 from __future__ import annotations
 
+import bisect
 import re
 import sqlite3
 import sys
@@ -33,7 +34,8 @@ def main() -> None:
     if len(ends) < 2:
         print("need two complete steps in the trace")
         return
-    lo, hi = ends[-2] + 1, ends[-1] + 1
+    # the last window whose AdamW run is followed by another step's forward (the overlapped update runs beside it)
+    lo, hi = (ends[-3] + 1, ends[-2] + 1) if len(ends) > 2 else (ends[-2] + 1, ends[-1] + 1)
     step = rows[lo:hi]
     tot = defaultdict(float)
     for name, s, e in step:
@@ -55,6 +57,32 @@ def main() -> None:
     # device time outside the window; tools/gap_summary.py measures idle time from a HIP API + kernel trace
     print(f"last complete step: {len(step)} kernels, kernel time {busy:.1f} ms, device busy (union) "
           f"{union / 1e6:.1f} ms, span {span:.1f} ms")
+    # how much of the optimizer update ran beside other kernels (the overlapped step's point): AdamW time covered by
+    # the union of every non-AdamW kernel interval of the whole trace
+    others, cur = [], None
+    for name, s, e in rows:
+        if "adamw" in name:
+            continue
+        if cur is None or s > cur[1]:
+            if cur is not None:
+                others.append(cur)
+            cur = [s, e]
+        else:
+            cur[1] = max(cur[1], e)
+    if cur is not None:
+        others.append(cur)
+    adam_win = [(s, e) for name, s, e in step if "adamw" in name]
+    starts = [o[0] for o in others]
+    cov = 0
+    for s, e in adam_win:
+        i = max(bisect.bisect_right(starts, s) - 1, 0)
+        while i < len(others) and others[i][0] < e:
+            cov += max(0, min(e, others[i][1]) - max(s, others[i][0]))
+            i += 1
+    adam_t = sum(e - s for s, e in adam_win)
+    if adam_win:
+        print(f"AdamW of the step: {adam_t / 1e6:.1f} ms kernel time, {cov / 1e6:.1f} ms of it beside other kernels; "
+              f"first AdamW {(adam_win[0][0] - step[0][1]) / 1e6:.1f} ms after the window start")
     print("| category | ms | % of busy |\n|---|---|---|")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"| {k} | {v:.1f} | {100 * v / busy:.1f} |")
