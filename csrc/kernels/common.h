@@ -103,6 +103,16 @@ template <> struct IO<_Float16> {
     __device__ static __forceinline__ void st(_Float16* p, int64_t i, float v) { p[i] = (_Float16)v; }
 };
 
+// 4-element vectors of a storage type and scalar conversions (bf16 as u16 bits, round to nearest even)
+template <typename T> struct Vec4 { typedef T type __attribute__((ext_vector_type(4))); };
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(u16 x) { return bf2f(x); }
+__device__ __forceinline__ float to_f32(_Float16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ u16 from_f32<u16>(float x) { return f2bf(x); }
+template <> __device__ __forceinline__ _Float16 from_f32<_Float16>(float x) { return (_Float16)x; }
+
 // 8 contiguous elements <-> 8 floats, 16 B (bf16/f16) or 32 B (f32) per lane.
 template <typename T> struct V8;
 template <> struct V8<u16> {

@@ -241,6 +241,19 @@ __device__ __forceinline__ bool drop_keep(uint32_t row, int ktok, uint32_t thr) 
     return mix32(row ^ ((uint32_t)ktok * 0x85ebca6bu)) >= thr;
 }
 
+// q head of grid column x (grid x = Hq, walked fastest, so x mod 8 is the workgroup's XCD: blockIdx round-robins
+// over the 8 XCDs).  With SA_ATTN_XCD each XCD takes Hq/8 CONSECUTIVE q heads, i.e. whole GQA groups, so the K / V
+// stream of a kv head is fetched into one XCD's L2 instead of Hq/Hkv of them (cdna_hip_programming.md T1).
+#ifndef SA_ATTN_XCD
+#define SA_ATTN_XCD 1
+#endif
+__device__ __forceinline__ int xcd_head(int x, int Hq) {
+    if constexpr (SA_ATTN_XCD) {
+        if ((Hq & 7) == 0) return (x & 7) * (Hq >> 3) + (x >> 3);
+    }
+    return x;
+}
+
 // row offset (r) of accumulator register j in a 32x32 MFMA C tile, excluding the 4h lane term
 __host__ __device__ constexpr int crow(int j) { return (j & 3) + 8 * (j >> 2); }
 

@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
-    const int seg = blockIdx.y, hq = blockIdx.x;  // grid (Hq, nseg, q tiles), heaviest tiles first
+    const int seg = blockIdx.y, hq = xcd_head(blockIdx.x, a.Hq);  // grid (Hq, nseg, q tiles), heaviest tiles first
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int ntiles_q = (Lq + 127) / 128;

@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
     // dimension and causal work is issued heaviest-first across all heads (LPT balance)
-    const int seg = blockIdx.y, hq = blockIdx.x;
+    const int seg = blockIdx.y, hq = xcd_head(blockIdx.x, a.Hq);
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int ntiles_q = (Lq + C::BM - 1) / C::BM;

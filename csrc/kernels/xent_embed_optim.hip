@@ -156,10 +156,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
         f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
         f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
         f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+        const auto gv = reinterpret_cast<const typename Vec4<G>::type*>(g)[i];  // one 8-B (16-B for f32) load
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float gr = IO<G>::ld(g, i * 4 + j) * gscale;
+            const float gr = to_f32(gv[j]) * gscale;
             float pp = pv[j] * decay;
             const float mm = b1 * mv[j] + (1.f - b1) * gr;
             const float vvv = b2 * vv[j] + (1.f - b2) * gr * gr;
@@ -170,8 +171,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
         reinterpret_cast<f32x4*>(m)[i] = mv;
         reinterpret_cast<f32x4*>(v)[i] = vv;
         if (pout) {
+            typename Vec4<P>::type ov;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) IO<P>::st(pout, i * 4 + j, o[j]);
+            for (int j = 0; j < 4; ++j) ov[j] = from_f32<P>(o[j]);
+            reinterpret_cast<typename Vec4<P>::type*>(pout)[i] = ov;
         }
     }
     // tail
@@ -291,7 +294,10 @@ void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* s
 void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, void* pout, int64_t n, float lr,
            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale, hipStream_t st) {
     if (n == 0) return;
-    const int vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) % 16) == 0;
+    // the vector path also loads 4 gradients / stores 4 parameters per access: g and pout 4-element aligned too
+    const int gsz = gdtype == DT_F32 ? 4 : 2, psz = pdtype == DT_F32 ? 4 : 2;
+    const int vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) % 16) == 0 &&
+                    reinterpret_cast<uintptr_t>(g) % (4 * gsz) == 0 && reinterpret_cast<uintptr_t>(pout) % (4 * psz) == 0;
     const int grid = gridn(vec ? n / 4 + 1 : n, 256, 8192);
 #define SA_ADAM(GT, PT) hipLaunchKernelGGL((adamw_kernel<GT, PT>), grid, 256, 0, st, p, (const GT*)g, m, v, (PT*)pout, n, lr, b1, b2, eps, wd, bc1, bc2_sqrt, gscale, vec)
     if (gdtype == DT_F32) {
