@@ -267,6 +267,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
 
     auto tile = [&](const char* K, int kt) {
+        // every key of the tile masked for every row of this wave: p = 0 throughout, the tile adds exactly nothing, so
+        // its MFMAs and softmax are skipped (wave-uniform; the wave still stages and barriers with the workgroup)
+        if ((a.causal && kt > qw0 + 31 + off) || (win >= 0 && kt + C::KT - 1 < qw0 + off - win) ||
+            (!a.causal && win >= 0 && kt > qw0 + 31 + off + win))
+            return;
         const char* V = K + C::TILE;
         f32x16 s[2] = {f32x16{}, f32x16{}};
         {
