@@ -275,10 +275,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         const float* DL = LS + 64;
         const int qt = qlo + qi * QT;
         const int win = (h0 + gi) < a.local_heads ? a.window : -1;
-        // every (key, query) pair of this wave's 32 keys x the tile's queries masked: nothing to add, skip (wave-uniform)
-        if ((a.causal && kw0 > qt + QT - 1 + off) || (win >= 0 && kw0 + 31 < qt + off - win) ||
-            (!a.causal && win >= 0 && kw0 > qt + QT - 1 + off + win))
-            return;
         uint32_t hs = 0;
         if constexpr (DROP) hs = drop_head(a.seed, h0 + gi);
         const bool need_mask = (a.causal && kw0 + 31 > qt + off) ||
@@ -503,10 +499,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
                                (win >= 0 && (kt < qw0 + 31 + off - win || (!a.causal && kt + 63 > qw0 + off + win)));
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int kb = kt + 32 * b;  // every key of the block masked for every query of this wave: skip
-            if ((a.causal && kb > qw0 + 31 + off) || (win >= 0 && kb + 31 < qw0 + off - win) ||
-                (!a.causal && win >= 0 && kb > qw0 + 31 + off + win))
-                continue;
             f32x16 s = f32x16{}, dp = f32x16{};
             {
 #pragma unroll

@@ -262,22 +262,14 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #pragma unroll
     for (int t = 0; t < C::NT; ++t) o[t] = f32x16{};
     float m = -INFINITY, l = 0.f;
-    bool m_final = false;  // wave-uniform: every row of the wave has a finite running max (the fast path's premise)
     const float c2 = a.scale_log2;
     uint32_t drow = 0;
     if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
 
     auto tile = [&](const char* K, int kt) {
-        // every key of the tile masked for every row of this wave: p = 0 throughout, the tile adds exactly nothing, so
-        // its MFMAs and softmax are skipped (wave-uniform; the wave still stages and barriers with the workgroup)
-        if ((a.causal && kt > qw0 + 31 + off) || (win >= 0 && kt + C::KT - 1 < qw0 + off - win) ||
-            (!a.causal && win >= 0 && kt > qw0 + 31 + off + win))
-            return;
         const char* V = K + C::TILE;
-        f32x16 s[2];
-        auto qk = [&]() {
-            s[0] = f32x16{};
-            s[1] = f32x16{};
+        f32x16 s[2] = {f32x16{}, f32x16{}};
+        {
 #pragma unroll
             for (int ks = 0; ks < C::NKS; ++ks)
 #pragma unroll
@@ -291,78 +283,51 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             }
-        };
+        }
         // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
         const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
                                (win >= 0 && (kt < qw0 + 31 + off - win ||
                                                   (!a.causal && kt + C::KT - 1 > qw0 + off + win)));
-        auto apply_mask = [&]() {
-            if (need_mask) {
-                mask_fence();
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
-                    int hi = Lk - 1 - base;
-                    if (a.causal) hi = min(hi, myq + off - base);
-                    else if (win >= 0) hi = min(hi, myq + off + win - base);
-                    const int lo = win >= 0 ? myq + off - win - base : -1;
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
-                }
-            }
-        };
-        // p = exp2(s c2 - m) in place and the row sum of this tile (the lane^32 half folded in)
-        auto softmax_p = [&](float nm) {
-            float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
-                    s[b][j] = p;
-                    rs[j & 3] += p;
-                }
-            // (the row sum as a fifth P.V product against all-ones was measured slower: attn_rowsum_mfma_ab_r4.log)
-            return sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
-        };
-        qk();
-        apply_mask();
-        // Fast path (every row of the wave has a finite running max): exponentiate against the current m at once, no
-        // row max.  A tile row sum <= 128 proves every p <= 128, i.e. no score exceeded m by more than 7 (log2 units),
-        // so the exact path below would not have moved m either (it moves m only past TH = 8): same bits.  A row sum
-        // above 128 (or inf / NaN) sends the wave to the exact path with S recomputed (rare after the first tiles).
-        float rsum = 0.f;
-        bool exact = !m_final;
-        if (!exact) {
-            rsum = softmax_p(-m);
-            if (__builtin_amdgcn_ballot_w64(!(rsum <= 128.f)) != 0) {
-                mask_fence();
-                exact = true;
-                qk();
-                apply_mask();
-            }
-        }
-        if (exact) {
+        if (need_mask) {
             mask_fence();
-            // two independent 16-element chains, one statement each (no hazard pads inside)
-            const float m0 = vmax16(s[0]), m1 = vmax16(s[1]);
-            const float mx = vmax3(m0, m1, m1);
-            const float mrow = max_xchg32(mx) * c2;
-            if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {
-                mask_fence();
-                const float mnew = fmaxf(m, mrow);
-                const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
-                l *= alpha;
 #pragma unroll
-                for (int t = 0; t < C::NT; ++t)
+            for (int b = 0; b < 2; ++b) {
+                const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
+                int hi = Lk - 1 - base;
+                if (a.causal) hi = min(hi, myq + off - base);
+                else if (win >= 0) hi = min(hi, myq + off + win - base);
+                const int lo = win >= 0 ? myq + off - win - base : -1;
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) o[t][j] *= alpha;
-                m = mnew;
+                for (int j = 0; j < 16; ++j) s[b][j] = (crow(j) <= hi && crow(j) >= lo) ? s[b][j] : -INFINITY;
             }
-            rsum = softmax_p(m == -INFINITY ? 0.f : -m);
-            m_final = __builtin_amdgcn_ballot_w64(m == -INFINITY) == 0;
         }
-        l += rsum;
+        // two independent 16-element chains, one statement each (no hazard pads inside)
+        const float m0 = vmax16(s[0]), m1 = vmax16(s[1]);
+        const float mx = vmax3(m0, m1, m1);
+        const float mrow = max_xchg32(mx) * c2;
+        if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {  // rare after the first tiles
+            mask_fence();
+            const float mnew = fmaxf(m, mrow);
+            const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m - mnew);
+            l *= alpha;
+#pragma unroll
+            for (int t = 0; t < C::NT; ++t)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) o[t][j] *= alpha;
+            m = mnew;
+        }
+        const float nm = m == -INFINITY ? 0.f : -m;
+        float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
+                s[b][j] = p;
+                rs[j & 3] += p;
+            }
+        // (the row sum as a fifth P.V product against all-ones was measured slower: profiles/attn_rowsum_mfma_ab_r4.log)
+        l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
         if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
 #pragma unroll
             for (int b = 0; b < 2; ++b)
