@@ -37,7 +37,10 @@ using fa::bf16x8;
 using fa::lds_s16x4;
 using fa::lds_void;
 
-constexpr int kGroupM = 8;
+#ifndef SA_WGRAD_GROUPM
+#define SA_WGRAD_GROUPM 8
+#endif
+constexpr int kGroupM = SA_WGRAD_GROUPM;  // M-tiles per tile group (the 32 tiles resident on an XCD: kGroupM x 32/kGroupM)
 constexpr int BK = 32;                  // k rows per ring slot
 constexpr int kImg = BK * 256 * 2;      // one operand image [32][256] bf16 = 16 KiB
 constexpr int kSlot = 2 * kImg;         // A + B
