@@ -37,10 +37,18 @@ using fa::bf16x8;
 using fa::lds_s16x4;
 using fa::lds_void;
 
-#ifndef SA_WGRAD_GROUPM
-#define SA_WGRAD_GROUPM 8
+// M-tiles per tile group (the 32 tiles resident on one XCD are group_m x 32/group_m, sharing A / B panels in its L2):
+// 4 for tall outputs (tm >= 2 tn: gate/up 86 x 16 tiles +2.6 %, LM head 125 x 16 +1.6 %), 8 otherwise (down 16 x 43:
+// 8 beats 4 by 1.2 %; 16 loses everywhere), profiles/wgrad_group_ab_r5.log.  SA_WGRAD_GROUPM pins it for an A/B.
+__host__ __device__ __forceinline__ int group_m(int tm, int tn) {
+#ifdef SA_WGRAD_GROUPM
+    (void)tm;
+    (void)tn;
+    return SA_WGRAD_GROUPM;
+#else
+    return tm >= 2 * tn ? 4 : 8;
 #endif
-constexpr int kGroupM = SA_WGRAD_GROUPM;  // M-tiles per tile group (the 32 tiles resident on an XCD: kGroupM x 32/kGroupM)
+}
 constexpr int BK = 32;                  // k rows per ring slot
 constexpr int kImg = BK * 256 * 2;      // one operand image [32][256] bf16 = 16 KiB
 constexpr int kSlot = 2 * kImg;         // A + B
@@ -90,9 +98,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
         k_lo = (unit % tail_split) * nk;
     }
     const int ns = 2 * nk, s_lo = 2 * k_lo;  // 32-deep k-steps of this block
-    const int group = kGroupM * tn;
-    const int first_m = (v / group) * kGroupM;
-    const int gm = min(tm - first_m, kGroupM);
+    const int gM = group_m(tm, tn);
+    const int group = gM * tn;
+    const int first_m = (v / group) * gM;
+    const int gm = min(tm - first_m, gM);
     const int within = v % group;
     const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
 
@@ -288,9 +297,10 @@ __global__ __launch_bounds__(256) void gemm_tn_combine_kernel(const float* __res
                                                               int M, int N, int full_blocks, int split, int beta) {
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int v = full_blocks + (int)blockIdx.x;
-    const int group = kGroupM * tn;
-    const int first_m = (v / group) * kGroupM;
-    const int gm = min(tm - first_m, kGroupM);
+    const int gM = group_m(tm, tn);
+    const int group = gM * tn;
+    const int first_m = (v / group) * gM;
+    const int gm = min(tm - first_m, gM);
     const int within = v % group;
     const int m0 = (first_m + within % gm) * 256, n0 = (within / gm) * 256;
     const int row = 4 * (int)blockIdx.y + (threadIdx.x >> 6), col = (threadIdx.x & 63) * 4;
