@@ -6,90 +6,49 @@ using namespace sa;
 
 // ------------------------------------------------------------------ SwiGLU
 // out[t, j] = rnd(silu(a[t, j])) * b[t, j]  (torch: silu(x) then * y, each rounded to the storage type)
-// Grid-stride over 16-B chunks, two chunks per thread per iteration with both chunks' loads issued before any math
-// (twice the bytes in flight per lane); the chunk -> (row, column) split in 32-bit arithmetic when the chunk count fits
-// (a 64-bit division is ~4x the instructions).
-template <bool SMALL>
-__device__ __forceinline__ void chunk_rc(int64_t i, int vpr, int64_t& r, int& c) {
-    if constexpr (SMALL) {
-        const uint32_t q = (uint32_t)i / (uint32_t)vpr;
-        r = q;
-        c = (int)((uint32_t)i - q * (uint32_t)vpr) * 8;
-    } else {
-        r = i / vpr;
-        c = (int)(i - r * vpr) * 8;
-    }
-}
-
-template <typename T, bool SMALL>
+template <typename T>
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T* __restrict__ a, const T* __restrict__ b, int64_t lda,
                                                          T* __restrict__ out, int64_t rows, int F) {
     const int vpr = F / 8;
     const int64_t n = rows * vpr;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 2 * stride) {
-        float av[2][8], bv[2][8];
-        int64_t r[2];
-        int c[2];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / vpr;
+        const int c = (int)(i - r * vpr) * 8;
+        float av[8], bv[8], o[8];
+        V8<T>::ld(a + r * lda + c, av);
+        V8<T>::ld(b + r * lda + c, bv);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t i = i0 + u * stride;
-            if (i < n) {
-                chunk_rc<SMALL>(i, vpr, r[u], c[u]);
-                V8<T>::ld(a + r[u] * lda + c[u], av[u]);
-                V8<T>::ld(b + r[u] * lda + c[u], bv[u]);
-            }
+        for (int j = 0; j < 8; ++j) {
+            const float s = av[j] / (1.f + __expf(-av[j]));
+            o[j] = rnd<T>(s) * bv[j];
         }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (i0 + u * stride >= n) continue;
-            float o[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float s = av[u][j] / (1.f + __expf(-av[u][j]));
-                o[j] = rnd<T>(s) * bv[u][j];
-            }
-            V8<T>::st(out + r[u] * F + c[u], o);
-        }
+        V8<T>::st(out + r * F + c, o);
     }
 }
 
-template <typename T, bool SMALL>
+template <typename T>
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ a,
                                                          const T* __restrict__ b, int64_t lda, T* __restrict__ da,
                                                          T* __restrict__ db, int64_t ldd, int64_t rows, int F) {
     const int vpr = F / 8;
     const int64_t n = rows * vpr;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 2 * stride) {
-        float g[2][8], av[2][8], bv[2][8];
-        int64_t r[2];
-        int c[2];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / vpr;
+        const int c = (int)(i - r * vpr) * 8;
+        float g[8], av[8], bv[8], oa[8], ob[8];
+        V8<T>::ld(dy + r * F + c, g);
+        V8<T>::ld(a + r * lda + c, av);
+        V8<T>::ld(b + r * lda + c, bv);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t i = i0 + u * stride;
-            if (i < n) {
-                chunk_rc<SMALL>(i, vpr, r[u], c[u]);
-                V8<T>::ld(dy + r[u] * F + c[u], g[u]);
-                V8<T>::ld(a + r[u] * lda + c[u], av[u]);
-                V8<T>::ld(b + r[u] * lda + c[u], bv[u]);
-            }
+        for (int j = 0; j < 8; ++j) {
+            const float sig = 1.f / (1.f + __expf(-av[j]));
+            const float s = av[j] * sig;
+            ob[j] = g[j] * rnd<T>(s);
+            const float ds = g[j] * bv[j];
+            oa[j] = ds * (sig * (1.f + av[j] * (1.f - sig)));
         }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (i0 + u * stride >= n) continue;
-            float oa[8], ob[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float sig = 1.f / (1.f + __expf(-av[u][j]));
-                const float s = av[u][j] * sig;
-                ob[j] = g[u][j] * rnd<T>(s);
-                const float ds = g[u][j] * bv[u][j];
-                oa[j] = ds * (sig * (1.f + av[u][j] * (1.f - sig)));
-            }
-            V8<T>::st(da + r[u] * ldd + c[u], oa);
-            V8<T>::st(db + r[u] * ldd + c[u], ob);
-        }
+        V8<T>::st(da + r * ldd + c, oa);
+        V8<T>::st(db + r * ldd + c, ob);
     }
 }
 
@@ -295,25 +254,17 @@ bool rope_kv_append(int dtype, bool interleaved, const void* x, void* q_out, voi
     return true;
 }
 void swiglu_fwd(int dtype, const void* a, const void* b, int64_t lda, void* out, int64_t rows, int F, hipStream_t st) {
-    const int64_t n = rows * (F / 8);
-    const int g = grid_for((n + 1) / 2);
-    const bool small = n < (int64_t(1) << 32);
-#define SA_SWF(TT, SM) hipLaunchKernelGGL((swiglu_fwd_kernel<TT, SM>), g, 256, 0, st, (const TT*)a, (const TT*)b, lda, (TT*)out, rows, F)
-    if (dtype == DT_BF16) { if (small) SA_SWF(u16, true); else SA_SWF(u16, false); }
-    else if (dtype == DT_F16) { if (small) SA_SWF(f16, true); else SA_SWF(f16, false); }
-    else { if (small) SA_SWF(float, true); else SA_SWF(float, false); }
-#undef SA_SWF
+    const int g = grid_for(rows * (F / 8));
+    if (dtype == DT_BF16) hipLaunchKernelGGL(swiglu_fwd_kernel<u16>, g, 256, 0, st, (const u16*)a, (const u16*)b, lda, (u16*)out, rows, F);
+    else if (dtype == DT_F16) hipLaunchKernelGGL(swiglu_fwd_kernel<f16>, g, 256, 0, st, (const f16*)a, (const f16*)b, lda, (f16*)out, rows, F);
+    else hipLaunchKernelGGL(swiglu_fwd_kernel<float>, g, 256, 0, st, (const float*)a, (const float*)b, lda, (float*)out, rows, F);
 }
 void swiglu_bwd(int dtype, const void* dy, const void* a, const void* b, int64_t lda, void* da, void* db, int64_t ldd,
                 int64_t rows, int F, hipStream_t st) {
-    const int64_t n = rows * (F / 8);
-    const int g = grid_for((n + 1) / 2);
-    const bool small = n < (int64_t(1) << 32);
-#define SA_SWB(TT, SM) hipLaunchKernelGGL((swiglu_bwd_kernel<TT, SM>), g, 256, 0, st, (const TT*)dy, (const TT*)a, (const TT*)b, lda, (TT*)da, (TT*)db, ldd, rows, F)
-    if (dtype == DT_BF16) { if (small) SA_SWB(u16, true); else SA_SWB(u16, false); }
-    else if (dtype == DT_F16) { if (small) SA_SWB(f16, true); else SA_SWB(f16, false); }
-    else { if (small) SA_SWB(float, true); else SA_SWB(float, false); }
-#undef SA_SWB
+    const int g = grid_for(rows * (F / 8));
+    if (dtype == DT_BF16) hipLaunchKernelGGL(swiglu_bwd_kernel<u16>, g, 256, 0, st, (const u16*)dy, (const u16*)a, (const u16*)b, lda, (u16*)da, (u16*)db, ldd, rows, F);
+    else if (dtype == DT_F16) hipLaunchKernelGGL(swiglu_bwd_kernel<f16>, g, 256, 0, st, (const f16*)dy, (const f16*)a, (const f16*)b, lda, (f16*)da, (f16*)db, ldd, rows, F);
+    else hipLaunchKernelGGL(swiglu_bwd_kernel<float>, g, 256, 0, st, (const float*)dy, (const float*)a, (const float*)b, lda, (float*)da, (float*)db, ldd, rows, F);
 }
 void rope(int dtype, bool interleaved, const void* x, int64_t x_tok, int64_t x_head, void* out, int64_t o_tok,
           int64_t o_head, const float* cosb, const float* sinb, const int64_t* pos, int64_t T_, int nh, int hd, int rd,
