@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     // work item (q head h0 + gi, query tile qlo + QT qi), qi fastest; the issue and compute cursors advance
     // incrementally (no runtime divisions in the loop)
     auto issue = [&](int gi, int qi, char* buf) {
-        const int qt = qlo + qi * QT, hq = h0 + gi;
+        const int qt = (SA_PROBE & 4) ? qlo : qlo + qi * QT, hq = (SA_PROBE & 4) ? h0 : h0 + gi;  // probe 4: first item
         dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
         dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
         if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
@@ -485,8 +485,9 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     //  hipcc's host pass treat the kernel as undefined and drop its launch stub)
 #define SA_DQ_ISSUE(KT, BUFP)                                                                          \
     do {                                                                                               \
-        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);                \
-        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + TILE, wave_u);         \
+        const int kp_ = (SA_PROBE & 4) ? klo : (KT); /* timing probe 4: always the first tile */        \
+        dma_load(tk, kbase + (int64_t)kp_ * a.k_tok, a.k_tok, Lk - kp_, (BUFP), wave_u);                 \
+        dma_load(tv, vbase + (int64_t)kp_ * a.v_tok, a.v_tok, Lk - kp_, (BUFP) + TILE, wave_u);          \
     } while (0)
     f32x16 dq[NT];
 #pragma unroll

@@ -243,8 +243,9 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     const u16* vbase = a.v + (int64_t)k0s * a.v_tok + (int64_t)hk * a.v_head;
 #define SA_FWD_ISSUE(KT, BUFP)                                                                          \
     do {                                                                                                \
-        dma_load(tk, kbase + (int64_t)(KT) * a.k_tok, a.k_tok, Lk - (KT), (BUFP), wave_u);                   \
-        dma_load(tv, vbase + (int64_t)(KT) * a.v_tok, a.v_tok, Lk - (KT), (BUFP) + C::TILE, wave_u);         \
+        const int kp_ = (SA_PROBE & 4) ? klo : (KT); /* timing probe 4: always the first tile (L2-resident) */ \
+        dma_load(tk, kbase + (int64_t)kp_ * a.k_tok, a.k_tok, Lk - kp_, (BUFP), wave_u);                    \
+        dma_load(tv, vbase + (int64_t)kp_ * a.v_tok, a.v_tok, Lk - kp_, (BUFP) + C::TILE, wave_u);          \
     } while (0)
 
     bf16x8 qf[C::NKS];
