@@ -5,7 +5,6 @@
 #include <c10/core/DeviceGuard.h>
 
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -651,22 +650,9 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
             a.rrd = (int)rope_dim; a.rseq = (int)rope_seq; a.ril = rope_interleaved ? 1 : 0;
         }
     }
-    if (T > 0 && a.nseg > 0) {
-        // dQ beside dK/dV on a pooled side stream (SCALING_AMD_FA_BWD_STREAMS, default on; never while the stream is
-        // being captured into a graph).  The current stream waits for it before returning, so every tensor used here
-        // (delta / lse2 / partials allocated on the current stream included) stays live for it.
-        const hipStream_t st = cur_stream();
-        hipStream_t st_dq = nullptr;
-        static const bool split = [] {
-            const char* e = std::getenv("SCALING_AMD_FA_BWD_STREAMS");
-            return e == nullptr || std::string(e) != "0";
-        }();
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (split && hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone)
-            st_dq = c10::hip::getStreamFromPool(false, q.device().index()).stream();
+    if (T > 0 && a.nseg > 0)
         sa_launch::fa_bwd(a, (const uint16_t*)o.data_ptr(), o.stride(0), o.stride(1), T, (int)D, (int)max_q, (int)max_k,
-                          q.scalar_type() == at::kHalf, st, st_dq);
-    }
+                          q.scalar_type() == at::kHalf, cur_stream());
     if (rope && !fold) {
         const int64_t* pp = rope_pos.has_value() ? rope_pos->data_ptr<int64_t>() : nullptr;
         for (at::Tensor* t : {&dq, &dk})

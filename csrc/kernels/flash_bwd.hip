@@ -594,27 +594,8 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
-// two reusable events per thread and device (the dQ stream's fork after the delta pass and its join)
-static void fork_join_events(hipEvent_t& fork, hipEvent_t& join) {
-    thread_local hipEvent_t ev[64][2] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (ev[dev][0] == nullptr) {
-        (void)hipEventCreateWithFlags(&ev[dev][0], hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&ev[dev][1], hipEventDisableTiming);
-    }
-    fork = ev[dev][0];
-    join = ev[dev][1];
-}
-
 template <bool F16, bool DROP>
-static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st, hipStream_t st_dq) {
-    hipEvent_t fork = nullptr, join = nullptr;
-    if (st_dq != nullptr) {
-        fork_join_events(fork, join);
-        (void)hipEventRecord(fork, st);  // delta / lse2 written
-        (void)hipStreamWaitEvent(st_dq, fork, 0);
-    }
+static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
@@ -625,14 +606,9 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
     {
         dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
-        hipStream_t sq = st_dq != nullptr ? st_dq : st;
-        if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, sq, a);
-        else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, sq, a);
-        else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, sq, a);
-    }
-    if (st_dq != nullptr) {
-        (void)hipEventRecord(join, st_dq);
-        (void)hipStreamWaitEvent(st, join, 0);
+        if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
+        else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
+        else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     if (a.hsplit > 1) {
         const int64_t threads = (int64_t)a.Tk * a.Hkv * (D / 8);
@@ -653,24 +629,24 @@ static void launch_bwd_dot(const BwdArgs& a, const uint16_t* o, int64_t o_tok, i
 
 template <int D>
 static void launch_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int max_q,
-                       int max_k, bool f16, hipStream_t st, hipStream_t st_dq) {
+                       int max_k, bool f16, hipStream_t st) {
     const bool drop = a.p_drop > 0.f;
     if (f16) {
         launch_bwd_dot<D, _Float16>(a, o, o_tok, o_head, Tq, st);
-        if (drop) launch_bwd_main<true, true>(a, D, max_q, max_k, st, st_dq);
-        else launch_bwd_main<true, false>(a, D, max_q, max_k, st, st_dq);
+        if (drop) launch_bwd_main<true, true>(a, D, max_q, max_k, st);
+        else launch_bwd_main<true, false>(a, D, max_q, max_k, st);
     } else {
         launch_bwd_dot<D, u16>(a, o, o_tok, o_head, Tq, st);
-        if (drop) launch_bwd_main<false, true>(a, D, max_q, max_k, st, st_dq);
-        else launch_bwd_main<false, false>(a, D, max_q, max_k, st, st_dq);
+        if (drop) launch_bwd_main<false, true>(a, D, max_q, max_k, st);
+        else launch_bwd_main<false, false>(a, D, max_q, max_k, st);
     }
 }
 
 namespace sa_launch {
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
-            bool f16, hipStream_t st, hipStream_t st_dq) {
-    if (D == 128) launch_bwd<128>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st, st_dq);
-    else if (D == 64) launch_bwd<64>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st, st_dq);
-    else launch_bwd<32>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st, st_dq);
+            bool f16, hipStream_t st) {
+    if (D == 128) launch_bwd<128>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
+    else if (D == 64) launch_bwd<64>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
+    else launch_bwd<32>(a, o, o_tok, o_head, Tq, max_q, max_k, f16, st);
 }
 }  // namespace sa_launch

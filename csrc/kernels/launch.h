@@ -132,10 +132,8 @@ struct BwdArgs {
     int rrd, rseq, ril;
 };
 namespace sa_launch {
-// st_dq != nullptr: the dQ kernel runs on that stream beside the dK/dV kernel (ordered after the delta pass on st, and
-// st waits for it before anything later), filling each kernel's causal tail with the other's work
 void fa_bwd(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, int D, int max_q, int max_k,
-            bool f16, hipStream_t st, hipStream_t st_dq = nullptr);
+            bool f16, hipStream_t st);
 }
 
 namespace sa_launch {
