@@ -74,6 +74,23 @@ __device__ __forceinline__ void mfma16_acc(f32x4& c, const bf16x8& a, const bf16
 __device__ __forceinline__ int sw16(int r) { return ((r & 3) << 2) ^ (((r >> 2) & 1) << 1); }
 __device__ __forceinline__ int koff16(int r, int c) { return r * 512 + 16 * ((c >> 3) ^ sw16(r)) + ((c & 7) << 1); }
 
+// Workgroup -> virtual tile id (the tile order of group_m above).  SA_WGRAD_ROUND (default): round-major -- the 256
+// workgroups resident at once (one per CU) take the contiguous range [256 r, 256 r + 256) of the tile order, a
+// compact chip-wide block whose panels shared across XCDs are served by the MALL, and XCD c (workgroups b % 8 == c)
+// its 32-tile sub-range, a compact block in that XCD's L2.  Otherwise the XCD-contiguous remap over the whole grid.
+#ifndef SA_WGRAD_ROUND
+#define SA_WGRAD_ROUND 1
+#endif
+__device__ __forceinline__ int round_remap(int b, int nwg) {
+    if constexpr (SA_WGRAD_ROUND) {
+        constexpr int R = 256;
+        const int full = nwg / R * R;
+        if (b >= full) return full + xcd_remap(b - full, nwg - full);
+        return b / R * R + xcd_remap(b % R, R);
+    }
+    return xcd_remap(b, nwg);
+}
+
 template <bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restrict__ A, int lda, uint32_t a_bytes,
                                                               const u16* __restrict__ B, int ldb, uint32_t b_bytes,
@@ -90,7 +107,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_ring_kernel(const u16* __restr
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     int v, k_lo = 0, nk = K / 64, unit = -1;  // 64-deep tiles (the split plan's unit)
     if ((int)blockIdx.x < full_blocks) {
-        v = xcd_remap(blockIdx.x, full_blocks);
+        v = round_remap(blockIdx.x, full_blocks);
     } else {
         unit = (int)blockIdx.x - full_blocks;
         v = full_blocks + unit / tail_split;
