@@ -260,6 +260,22 @@ __device__ __forceinline__ int xcd_head(int x, int Hq) {
     return x;
 }
 
+// Grid of the query-tiled kernels (forward, dQ): x = q head (xcd_head), and (SA_ATTN_SEGMAJOR, default) y = query
+// tile, z = segment, so the workgroups resident on an XCD at once are mostly the q tiles of few segments: they stream
+// the same K / V tiles in lockstep (one L2 fetch, many readers).  Otherwise y = segment, z = query tile (tile slowest).
+// Causal work is issued heaviest tile first either way (within a segment for the segment-major order).
+#ifndef SA_ATTN_SEGMAJOR
+#define SA_ATTN_SEGMAJOR 1
+#endif
+__host__ __device__ inline dim3 attn_grid(int hq, int nseg, int qtiles) {
+    return SA_ATTN_SEGMAJOR ? dim3(hq, qtiles, nseg) : dim3(hq, nseg, qtiles);
+}
+__device__ __forceinline__ int attn_seg() { return SA_ATTN_SEGMAJOR ? (int)blockIdx.z : (int)blockIdx.y; }
+__device__ __forceinline__ int attn_qtile(bool causal) {
+    const int n = SA_ATTN_SEGMAJOR ? (int)gridDim.y : (int)gridDim.z, i = SA_ATTN_SEGMAJOR ? (int)blockIdx.y : (int)blockIdx.z;
+    return causal ? n - 1 - i : i;
+}
+
 // row offset (r) of accumulator register j in a 32x32 MFMA C tile, excluding the 4h lane term
 __host__ __device__ constexpr int crow(int j) { return (j & 3) + 8 * (j >> 2); }
 

@@ -434,11 +434,11 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int TILE = 64 * D * 2, NKS = D / 16, NT = D / 32;
-    const int seg = blockIdx.y, hq = xcd_head(blockIdx.x, a.Hq);  // grid (Hq, nseg, q tiles), heaviest tiles first
+    const int seg = attn_seg(), hq = xcd_head(blockIdx.x, a.Hq);  // see attn_grid
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int ntiles_q = (Lq + 127) / 128;
-    const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
+    const int qt = attn_qtile(a.causal);
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
     const int win = hq < a.local_heads ? a.window : -1;
@@ -604,7 +604,7 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     {
-        dim3 grid(a.Hq, a.nseg, (max_q + 127) / 128);
+        dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + 127) / 128);
         const size_t lds = 4 * 64 * D * 2;
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);

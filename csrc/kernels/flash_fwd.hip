@@ -199,11 +199,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
     // dimension and causal work is issued heaviest-first across all heads (LPT balance)
-    const int seg = blockIdx.y, hq = xcd_head(blockIdx.x, a.Hq);
+    const int seg = attn_seg(), hq = xcd_head(blockIdx.x, a.Hq);  // see attn_grid
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
     const int ntiles_q = (Lq + C::BM - 1) / C::BM;
-    const int qt = a.causal ? (int)gridDim.z - 1 - (int)blockIdx.z : (int)blockIdx.z;
+    const int qt = attn_qtile(a.causal);
     if (qt >= ntiles_q) return;
     const int hk = hq / (a.Hq / a.Hkv);
     const int win = hq < a.local_heads ? a.window : -1;  // per-head window (mixed local/global heads)
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
-        dim3 grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(256);
+        dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(256);
         if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
         else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
         return;
