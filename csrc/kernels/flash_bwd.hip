@@ -14,12 +14,6 @@
 using namespace sa;
 using namespace sa::fa;
 
-// dK/dV grid order: SA_DKDV_SEGMAJOR = (kv head x split, key block, segment), the key blocks of few segments resident
-// together; 0 = (kv head x split, segment, key block), key block slowest (heaviest first across every segment)
-#ifndef SA_DKDV_SEGMAJOR
-#define SA_DKDV_SEGMAJOR 0
-#endif
-
 // race forensics: pad between the last MFMAs of a kernel and its epilogue's reads of their accumulators
 #ifndef SA_FA_BWD_EPI_PAD
 #define SA_FA_BWD_EPI_PAD 0
@@ -208,12 +202,12 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int QT = 32, TILE = QT * D * 2, BUF = 2 * TILE + 512, VIMG = 128 * D * 2, NKS = D / 16, NT = D / 32;
-    // grid (Hkv * hsplit, nseg, key blocks): key block slowest so causal work is issued heaviest-first
-    const int seg = SA_DKDV_SEGMAJOR ? (int)blockIdx.z : (int)blockIdx.y, hk = blockIdx.x / a.hsplit,
-              sub = blockIdx.x % a.hsplit;
+    // grid (Hkv * hsplit, nseg, key blocks): key block slowest so causal work is issued heaviest-first (a segment-major
+    // order, the forward's choice, measured 7 % slower here: profiles/attn_segmajor_ab_r5.log)
+    const int seg = blockIdx.y, hk = blockIdx.x / a.hsplit, sub = blockIdx.x % a.hsplit;
     const int q0s = a.cu_q[seg], k0s = a.cu_k[seg];
     const int Lq = a.cu_q[seg + 1] - q0s, Lk = a.cu_k[seg + 1] - k0s;
-    const int kwg0 = (SA_DKDV_SEGMAJOR ? (int)blockIdx.y : (int)blockIdx.z) * 128;
+    const int kwg0 = blockIdx.z * 128;
     if (kwg0 >= Lk) return;
     const int grp = a.Hq / a.Hkv / a.hsplit;  // q heads swept by this workgroup: hk * Hq/Hkv + sub * grp + [0, grp)
     const int h0 = hk * (a.Hq / a.Hkv) + sub * grp;
@@ -604,8 +598,7 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
-        const int kb = (max_k + 127) / 128;
-        dim3 grid = SA_DKDV_SEGMAJOR ? dim3(a.Hkv * a.hsplit, kb, a.nseg) : dim3(a.Hkv * a.hsplit, a.nseg, kb);
+        dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
         const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
