@@ -15,9 +15,15 @@ iters = int(os.environ.get("ITERS", 5))
 CAUSAL = os.environ.get("CAUSAL", "1") != "0"
 T = B * S
 cu = torch.arange(0, T + 1, S, device="cuda", dtype=torch.int32)
-q = torch.randn(T, HQ, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-k = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-v = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+if os.environ.get("PACKED") == "1":  # q / k / v as views of one [T, Hq + 2 Hkv, D] projection output, as in training
+    base = torch.randn(T, HQ + 2 * HK, D, device="cuda", dtype=torch.bfloat16)
+    q = base[:, :HQ].detach().requires_grad_(True)
+    k = base[:, HQ:HQ + HK].detach().requires_grad_(True)
+    v = base[:, HQ + HK:].detach().requires_grad_(True)
+else:
+    q = torch.randn(T, HQ, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(T, HK, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 g = torch.randn(T, HQ, D, device="cuda", dtype=torch.bfloat16)
 sc = 1 / math.sqrt(D)
 
