@@ -35,10 +35,6 @@
 
 using namespace sa;
 
-#ifndef SA_NT_ROUND
-#define SA_NT_ROUND 1
-#endif
-
 namespace sa_gemm_nt {
 
 using fa::bf16x8;
@@ -76,15 +72,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(const u16* __restrict__
     // of GM M-tiles sweeping N together (4 beat 8 / 16: profiles/gemm_nt_group_ab_r4.log)
     constexpr int GM = 4;
     auto tile_of = [&](int vb, int& tm0, int& tnt) {
-        // SA_NT_ROUND (default): round-major -- the G workgroups' k-th tiles (virtual blocks [kG, kG + G)) form a compact
-        // chip-wide block and each XCD's share a compact sub-block (as the weight-gradient GEMM's round_remap)
-        int v;
-        if constexpr (SA_NT_ROUND) {
-            const int G = (int)gridDim.x, full = ntiles / G * G;
-            v = vb >= full ? full + xcd_remap(vb - full, ntiles - full) : vb / G * G + xcd_remap(vb % G, G);
-        } else {
-            v = xcd_remap(vb, ntiles);
-        }
+        const int v = xcd_remap(vb, ntiles);
         const int group = GM * tn;
         const int first_m = (v / group) * GM;
         const int gm = min(tm - first_m, GM);
