@@ -10,9 +10,8 @@ from typing import Callable, Optional
 
 import torch
 
-from ....core import ColumnParallelLinear, Topology, VocabParallelEmbedding
-from ....core.nn.linear.utils import all_concat, copy_to_tensor_model_parallel_region
-from ....ops.gemm import linear as gemm_linear
+from ....core import ColumnParallelLinear, Topology
+from ....core.nn.linear.utils import all_concat
 from ...context.config import TransformerArchitectureConfig
 from .base import TransformerLayerBaseIO, TransformerLayerIO
 from .embedding import _device
@@ -55,22 +54,4 @@ class TransformerLMHead(TransformerLayerBaseIO):
         return _finish(self, x, self.linear(x.activations), self.vocab_per_rank)
 
 
-class TransformerLMHeadTied(TransformerLayerBaseIO):
-    def __init__(self, architecture_config: TransformerArchitectureConfig,
-                 init_method: Callable[[torch.Tensor], torch.Tensor] = torch.nn.init.xavier_normal_,
-                 topology: Optional[Topology] = None):
-        super().__init__()
-        cfg = architecture_config
-        self.topology = topology
-        self.embedding = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, topology=topology,
-                                                device=None if topology is not None else _device(topology),
-                                                dtype=cfg.precision.dtype, init_method=init_method,
-                                                finetunable_token_ids=cfg.finetunable_token_ids)
-        tp = 1 if topology is None else topology.config.model_parallel_size
-        self.vocab_per_rank = cfg.vocab_size // tp
-
-    def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
-        act = x.activations
-        if self.topology is not None and self.topology.config.model_parallel_size > 1:
-            act = copy_to_tensor_model_parallel_region(act, topology=self.topology)
-        return _finish(self, x, gemm_linear(act, self.embedding.weight), self.vocab_per_rank)
+from .lm_head_tied import TransformerLMHeadTied  # noqa: E402,F401  (re-export)
