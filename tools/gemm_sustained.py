@@ -12,7 +12,12 @@ import argparse
 import json
 import time
 
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {  # (tokens, in, out) of F.linear(x[tokens, in], W[out, in])
     "qkv": (32768, 4096, 6144),

@@ -11,7 +11,12 @@ from __future__ import annotations
 import json
 import statistics
 
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
 
