@@ -13,9 +13,6 @@
 using namespace sa;
 using namespace sa::fa;
 
-#ifndef SA_FWD_PRIO
-#define SA_FWD_PRIO 0
-#endif
 template <int D, bool F16, bool DROP>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
@@ -288,9 +285,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             }
         }
-        // A/B hook (off): SA_FWD_PRIO 1 raises the wave's issue priority over its softmax VALU, 2 over its MFMA phases
-        if constexpr (SA_FWD_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-        if constexpr (SA_FWD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         // wave-uniform: does any element of this wave's 32 x 64 block need a mask?
         const bool need_mask = (kt + C::KT > Lk) || (a.causal && kt + C::KT - 1 > qw0 + off) ||
                                (win >= 0 && (kt < qw0 + 31 + off - win ||
@@ -347,8 +341,6 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
-        if constexpr (SA_FWD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-        if constexpr (SA_FWD_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         {
 #pragma unroll
             for (int t = 0; t < C::NT; ++t)
