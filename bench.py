@@ -75,9 +75,10 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--lora-rank", type=int, default=64)
     p.add_argument("--preset", type=str, default=None, choices=sorted(PRESETS),
                    help="BASELINE.json layouts: baseline3 = TP2 x DP(N/2) ZeRO-1 + SP, baseline4 = TP2 x PP2 x DP(N/4) "
-                        "1F1B + activation checkpointing + SP, baseline5 = LoRA TP1 x DP(N) ZeRO-1 (overrides the "
-                        "layout flags it names; see PRESETS)")
-    p.add_argument("--shard-proxy", type=str, default=None, choices=["baseline3", "baseline4"],
+                        "1F1B + every_layer activation checkpointing + SP (baseline4_save_matmuls: the same with the "
+                        "selective recompute), baseline5 = LoRA TP1 x DP(N) ZeRO-1 (overrides the layout flags it "
+                        "names; see PRESETS)")
+    p.add_argument("--shard-proxy", type=str, default=None, choices=["baseline3", "baseline4", "baseline4_save_matmuls"],
                    help="1-GPU per-rank proxy of an 8-GPU preset: ONE process runs rank 0's tensor-parallel shard "
                         "(TP2: 16 q / 4 kv heads, SwiGLU 5504, vocab 16000) of one pipeline stage's layers (baseline4: "
                         "16) with the preset's micro-batching, sequence parallelism and checkpointing; collectives are "
@@ -103,12 +104,16 @@ PRESETS: dict[str, dict[str, Any]] = {
     # instead of all-reduce, activations sharded), row-parallel GEMMs overlapped with their collective in 4 pieces
     "baseline3": {"tp": 2, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": True, "tp_comm_chunks": 0,
                   "activation_checkpointing": "disabled", "lora": False, "zero": 1},
-    # "TP=2 PP=2 DP=2 (full 3D parallel, 1F1B pipeline) with activation checkpointing": 4 micro-batches of 4 keep the
-    # two-stage pipe 4/5 busy; checkpointing per layer in the mode that keeps the GEMM outputs (the recompute runs only
-    # the element-wise work): per-rank proxy 626 ms/step vs 583 without checkpointing (+7.4 %, 39.0 vs 45.7 GiB) and
-    # 807 ms for the reference's every_layer (+38 %, 30.8 GiB) -- profiles/proxy_baseline4_ac_r5.log
+    # "TP=2 PP=2 DP=2 (full 3D parallel, 1F1B pipeline) with activation checkpointing": the reference's per-layer
+    # checkpointing (every_layer).  Micro-batching: see profiles/proxy_baseline4_mb_r6.md
     "baseline4": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True, "tp_comm_chunks": 0,
-                  "activation_checkpointing": "every_layer_save_matmuls", "lora": False, "zero": 1},
+                  "activation_checkpointing": "every_layer", "lora": False, "zero": 1},
+    # the same layout with this framework's selective recompute (every_layer_save_matmuls keeps every GEMM output, the
+    # recompute runs only the element-wise work): per-rank proxy 626 ms/step vs 807 for every_layer, 39.0 vs 30.8 GiB
+    # (profiles/proxy_baseline4_ac_r5.log).  A labelled variant, not BASELINE #4's checkpointing semantics
+    "baseline4_save_matmuls": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True,
+                               "tp_comm_chunks": 0, "activation_checkpointing": "every_layer_save_matmuls",
+                               "lora": False, "zero": 1},
     # "7B + LoRA fine-tune path, TP=1 PP=1 DP=8 ZeRO-1 (PEFT adapters exercised)"
     "baseline5": {"tp": 1, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": False, "tp_comm_chunks": 1,
                   "activation_checkpointing": "disabled", "lora": True, "zero": 1},
@@ -177,6 +182,24 @@ def _free_port() -> int:
     return find_free_port()
 
 
+def _visible_devices() -> int:
+    """GPU count without initialising the GPU (torch.cuda.device_count() does not; 1 when torch cannot tell)."""
+    try:
+        import torch
+
+        return max(1, torch.cuda.device_count())
+    except Exception:  # noqa: BLE001 - launcher on a host without torch GPU support
+        return 1
+
+
+def _rehearsal_slot(rank: int, world: int, ndev: Optional[int] = None) -> tuple[int, int, int]:
+    """(device, index among the ranks on that device, ranks on that device) of a rehearsal rank: ranks are dealt over
+    the visible devices round-robin (rank % ndev, as Topology.device places them)."""
+    n = ndev or _visible_devices()
+    dev = rank % n
+    return dev, rank // n, len(range(dev, world, n))
+
+
 def _launch(a: argparse.Namespace) -> int:
     """Spawns one worker per GPU (this file, with the rank env set); fail-fast on the first bad exit."""
     port = os.environ.get("MASTER_PORT") or str(_free_port())
@@ -187,14 +210,15 @@ def _launch(a: argparse.Namespace) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if a.backend == "gloo":  # CPU ranks: do not oversubscribe the host's cores
             env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // a.gpus)))
-        # rehearsal ranks sharing one GPU: each on a disjoint CU range, as it would own a GPU (value: the device's CU
-        # count, "1" = MI355X's 256).  Waves of two ranks co-resident on one CU made ~0.2-1 % of attention backwards
-        # differ by <= 1 bf16 ulp from a recomputation in place; 0 of 768 with the split (profiles/race_forensics_r5.md)
+        # optional: rehearsal ranks sharing a GPU each on a disjoint CU range, as each would own a GPU (value: the
+        # device's CU count, "1" = MI355X's 256).  Rank r runs on device r % ndev (Topology.device), so the mask names
+        # that device and splits its CUs among the ranks placed on it
         split = os.environ.get("SCALING_AMD_REHEARSAL_CU_SPLIT", "0") or "0"
         cus = 256 if split == "1" else int(split)
         if a.backend == "gloo-gpu" and cus and a.gpus > 1:
-            per = cus // a.gpus
-            env["HSA_CU_MASK"] = f"0:{r * per}-{(r + 1) * per - 1}"
+            dev, slot, per_dev = _rehearsal_slot(r, a.gpus)
+            per = cus // per_dev
+            env["HSA_CU_MASK"] = f"{dev}:{slot * per}-{(slot + 1) * per - 1}"
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
 
     def _kill_all(sig: int) -> None:
@@ -344,6 +368,12 @@ def _worker(a: argparse.Namespace) -> None:
     from scaling_amd.utils.gemm_tuning import enable_tuned_gemms
 
     gpu = a.backend != "gloo"
+    # forensics / A-B instrumentation kept outside the production code (e.g. tools/attn_forensics.py): each listed file
+    # is executed once here, before the model is built, and may wrap framework functions
+    for hook in filter(None, os.environ.get("SCALING_AMD_DEBUG_HOOKS", "").split(",")):
+        import runpy
+
+        runpy.run_path(hook)
     if os.environ.get("SCALING_AMD_DETERMINISTIC") == "1":  # library-side determinism (race-check forensics)
         from scaling_amd.core.utils.debug_env import DETERMINISTIC_ENV, apply
 

@@ -476,52 +476,6 @@ void gemm_tn(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C, bool
                        ws_floats > 0 ? ws.data_ptr<float>() : nullptr);
 }
 
-// ---- gemm_nt.hip: 64-deep staged NT GEMM with fused epilogues (forward / input gradient of linear layers)
-static bool nt_operand(const at::Tensor& t) {
-    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 &&
-           (uintptr_t)t.data_ptr() % 16 == 0;
-}
-static bool nt_out(const at::Tensor& t, int64_t rows, int64_t cols) {
-    return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 && t.size(0) == rows &&
-           t.size(1) == cols && t.stride(0) % 4 == 0 && (uintptr_t)t.data_ptr() % 8 == 0;
-}
-bool gemm_nt_ok(const at::Tensor& A, const at::Tensor& B) {
-    return nt_operand(A) && nt_operand(B) && A.size(1) == B.size(1) && A.device() == B.device() &&
-           sa_launch::gemm_nt_supported(A.size(0), B.size(0), A.size(1), A.stride(0), B.stride(0));
-}
-void gemm_nt(const at::Tensor& A, const at::Tensor& B, const at::Tensor& C) {
-    TORCH_CHECK(gemm_nt_ok(A, B) && nt_out(C, A.size(0), B.size(0)), "gemm_nt: unsupported operands");
-    const at::DeviceGuard g(A.device());
-    NtEpi ep{(uint16_t*)C.data_ptr(), C.stride(0), nullptr, 0, nullptr, 0, 0};
-    sa_launch::gemm_nt(EPI_STORE, A.data_ptr(), A.stride(0), B.data_ptr(), B.stride(0), A.size(0), B.size(0),
-                         A.size(1), ep, cur_stream());
-}
-// x [M, K] @ [W_gate; W_up]^T ([2F, K]) -> h = silu(g) * u [M, F] and (if given) z = [g | u] [M, 2F]
-bool gemm_nt_swiglu_ok(const at::Tensor& A, const at::Tensor& W) {
-    return gemm_nt_ok(A, W) && W.size(0) % 256 == 0;
-}
-void gemm_nt_swiglu(const at::Tensor& A, const at::Tensor& W, const c10::optional<at::Tensor>& z, const at::Tensor& h) {
-    TORCH_CHECK(gemm_nt_swiglu_ok(A, W), "gemm_nt_swiglu: unsupported operands");
-    const int64_t F = W.size(0) / 2;
-    TORCH_CHECK(nt_out(h, A.size(0), F), "gemm_nt_swiglu: h must be [M, F] bf16");
-    TORCH_CHECK(!z.has_value() || nt_out(*z, A.size(0), 2 * F), "gemm_nt_swiglu: z must be [M, 2F] bf16");
-    const at::DeviceGuard g(A.device());
-    NtEpi ep{z.has_value() ? (uint16_t*)z->data_ptr() : nullptr, z.has_value() ? z->stride(0) : 0,
-             (uint16_t*)h.data_ptr(), h.stride(0), nullptr, 0, (int)F};
-    sa_launch::gemm_nt(EPI_SWIGLU, A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), A.size(0), W.size(0),
-                         A.size(1), ep, cur_stream());
-}
-// dY [M, H] @ Wt^T (Wt = W_down^T [F, H]) = dh, consumed in registers: dz = swiglu_bwd(dh, z) [M, 2F]
-void gemm_nt_swiglu_bwd(const at::Tensor& A, const at::Tensor& Wt, const at::Tensor& z, const at::Tensor& dz) {
-    TORCH_CHECK(gemm_nt_ok(A, Wt), "gemm_nt_swiglu_bwd: unsupported operands");
-    const int64_t F = Wt.size(0);
-    TORCH_CHECK(nt_out(z, A.size(0), 2 * F) && nt_out(dz, A.size(0), 2 * F), "gemm_nt_swiglu_bwd: z/dz must be [M, 2F]");
-    const at::DeviceGuard g(A.device());
-    NtEpi ep{(uint16_t*)dz.data_ptr(), dz.stride(0), nullptr, 0, (const uint16_t*)z.data_ptr(), z.stride(0), (int)F};
-    sa_launch::gemm_nt(EPI_SWIGLU_BWD, A.data_ptr(), A.stride(0), Wt.data_ptr(), Wt.stride(0), A.size(0), F,
-                         A.size(1), ep, cur_stream());
-}
-
 // ------------------------------------------------------------------ flash attention
 void check_qkv(const at::Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.dim() == 3 && t.stride(2) == 1, "flash_attn: ", n, " must be [T, heads, D] with unit last stride");
@@ -751,11 +705,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");
     m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
-    m.def("gemm_nt_ok", &gemm_nt_ok, "whether gemm_nt supports these operands");
-    m.def("gemm_nt", &gemm_nt, "C = A @ B^T (bf16, 64-deep staged HIP kernel)");
-    m.def("gemm_nt_swiglu_ok", &gemm_nt_swiglu_ok, "whether gemm_nt_swiglu supports these operands");
-    m.def("gemm_nt_swiglu", &gemm_nt_swiglu, "h = silu(g) u, z = [g | u] from x @ [W_gate; W_up]^T (one kernel)");
-    m.def("gemm_nt_swiglu_bwd", &gemm_nt_swiglu_bwd, "dz = swiglu_bwd(dY @ Wt^T, z) (one kernel)");
     m.def("ar_alloc", &ar_alloc, "one-shot all-reduce: allocate + IPC-export a registered buffer");
     m.def("ar_open", &ar_open, "one-shot all-reduce: map a peer's registered buffer");
     m.def("ar_close", &ar_close, "unmap a peer buffer");

@@ -123,7 +123,7 @@ template <int D, int W, int ROWS = 64>
 struct DmaTile {
     static constexpr int PIECES = ROWS * D * 2 / 1024;
     static constexpr int NPW = (PIECES + W - 1) / W;
-    static_assert(PIECES >= 1 && (PIECES % W == 0 || PIECES < W), "tile pieces must split evenly across waves");
+    static_assert(PIECES >= 1, "empty tile");
     int voff[NPW];
     __device__ __forceinline__ void init(int wave, int lane, int64_t tok) {
 #pragma unroll
@@ -138,7 +138,7 @@ struct DmaTile {
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(base, (uint32_t)max(rows, 0) * (uint32_t)tok * 2u);
 #pragma unroll
         for (int i = 0; i < NPW; ++i)
-            if (PIECES >= W || wave_u + W * i < PIECES)  // wave-uniform
+            if (PIECES % W == 0 || wave_u + W * i < PIECES)  // wave-uniform
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(tile + (wave_u + W * i) * 1024), 16, voff[i], 0, 0, 0);
     }
 };
@@ -274,6 +274,43 @@ __device__ __forceinline__ int attn_seg() { return SA_ATTN_SEGMAJOR ? (int)block
 __device__ __forceinline__ int attn_qtile(bool causal) {
     const int n = SA_ATTN_SEGMAJOR ? (int)gridDim.y : (int)gridDim.z, i = SA_ATTN_SEGMAJOR ? (int)blockIdx.y : (int)blockIdx.z;
     return causal ? n - 1 - i : i;
+}
+
+// Shared by the attention kernels: per-lane LDS offsets of row fragments (row lk, cols 16ks + 8h) and of
+// transposed fragments (rows 4h + i/4 (+8), cols 32t + 16g + 4(i&3)); tile bases and the 32/16-row
+// block offsets are compile-time immediates (loops unrolled per buffer).
+template <int D>
+struct LdsOffsets {
+    // swz(r, c) = c ^ F(r): a chunk index 2ks + h (row reads) or 4t + low (transposed reads) XOR F(r)
+    // splits into a per-lane base plus (const ^ per-lane high bits), so 6 registers replace 16 offsets
+    int row_base, row_hi;
+    int tr_base[2], tr_hi[2];
+    __device__ __forceinline__ void init(int lane) {
+        const int h = lane >> 5, r = lane & 31, g = (lane >> 4) & 1, i = lane & 15;
+        const int fr = swz<D>(r, 0);
+        row_base = r * D * 2 + 16 * (h ^ (fr & 1));
+        row_hi = 16 * (fr & ~1);
+        const int low = 2 * g + ((i & 3) >> 1);
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const int tr_row = 4 * h + (i >> 2) + 8 * x;
+            const int ft = swz<D>(tr_row, 0);
+            tr_base[x] = tr_row * D * 2 + 16 * (low ^ (ft & 3)) + (((4 * (i & 3)) & 7) << 1);
+            tr_hi[x] = 16 * (ft & ~3);
+        }
+    }
+    __device__ __forceinline__ int row(int ks) const { return row_base + ((32 * ks) ^ row_hi); }
+    __device__ __forceinline__ int tr(int t, int x) const { return tr_base[x] + ((64 * t) ^ tr_hi[x]); }
+};
+template <int D>
+__device__ __forceinline__ bf16x8 rd_row(const char* tile, int imm, int off) {
+    return *reinterpret_cast<const bf16x8*>(tile + imm + off);
+}
+template <int D>
+__device__ __forceinline__ bf16x8 rd_tr(const char* tile, int imm, const LdsOffsets<D>& lo, int t) {
+    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + lo.tr(t, 0)));
+    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + imm + lo.tr(t, 1)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // row offset (r) of accumulator register j in a 32x32 MFMA C tile, excluding the 4h lane term

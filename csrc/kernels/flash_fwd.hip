@@ -192,10 +192,14 @@ struct FwdV2 {
 // Variants measured against this one and dropped (8 waves per workgroup, inline-asm LDS-DMA, pinned read-ahead, an
 // 8-wave ping-pong schedule): profiles/attn_fwd_waves_ab_r2.log, attn_fwd_pingpong_ab_r3.log, attn_ab_r2_asyncdma.log;
 // their code is in git history before commit "Delete losing attention variants".
-template <int D, bool F16, bool DROP>
-__global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
+// NW = 4: 2 workgroups / CU = 2 waves / SIMD; NW = 6 (BM = 192): 2 workgroups / CU = 3 waves / SIMD (<= 168 VGPRs)
+#ifndef SA_FWD_NW
+#define SA_FWD_NW 4
+#endif
+template <int D, bool F16, bool DROP, int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
-    using C = FwdV2<D>;
+    using C = FwdV2<D, NW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
     // dimension and causal work is issued heaviest-first across all heads (LPT balance)
@@ -222,18 +226,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
     klo = (klo / C::KT) * C::KT;
 
     // ---- per-lane LDS offsets (bytes, relative to a tile base) ----
-    int rowoff[C::NKS];  // K row fragment: row lq, cols 16ks + 8h
-#pragma unroll
-    for (int ks = 0; ks < C::NKS; ++ks) rowoff[ks] = lds_off<D>(lq, 16 * ks + 8 * h);
-    int troff[C::NT][2];  // V^T fragment (ld_tr): rows 4h + i/4 (+8), cols 32t + 16g + 4(i&3)
-    {
-        const int g = (lane >> 4) & 1, i = lane & 15;
-#pragma unroll
-        for (int t = 0; t < C::NT; ++t) {
-            troff[t][0] = lds_off<D>(4 * h + (i >> 2), 32 * t + 16 * g + 4 * (i & 3));
-            troff[t][1] = lds_off<D>(4 * h + (i >> 2) + 8, 32 * t + 16 * g + 4 * (i & 3));
-        }
-    }
+    // per-lane LDS offsets: K row fragments (row lq, cols 16ks + 8h) and V^T fragments (rows 4h + i/4 (+8), cols
+    // 32t + 16g + 4(i&3)) as 6 registers + per-use XORs (a 16-register table spilled at 3 waves / SIMD)
+    LdsOffsets<D> lo;
+    lo.init(lane);
     // K / V tiles by LDS-DMA (no staging registers); rows past the segment land as zeros
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     DmaTile<D, C::NW> tk, tv;
@@ -275,7 +271,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
             for (int ks = 0; ks < C::NKS; ++ks)
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
-                    s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + rowoff[ks]), qf[ks], s[b]);
+                    s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + lo.row(ks)), qf[ks], s[b]);
             // one K fragment read per MFMA.  Reading them 4 MFMAs ahead (or interleaving the softmax of the previous
             // tile into these MFMAs) was measured slower: at two waves per SIMD the loop is bound by the SIMD's issue
             // slots, not by LDS latency (profiles/attn_sched_ab_r4.log)
@@ -349,8 +345,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #pragma unroll
                     for (int ss = 0; ss < 2; ++ss) {
                         const int kb = (32 * b + 16 * ss) * D * 2;
-                        const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][0]));
-                        const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + troff[t][1]));
+                        const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + lo.tr(t, 0)));
+                        const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(V + kb + lo.tr(t, 1)));
                         o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
                     }
 #pragma unroll
@@ -399,9 +395,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_v2_kernel(FwdArgs a) {
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
-        dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + FwdV2<128>::BM - 1) / FwdV2<128>::BM), block(256);
-        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP>), grid, block, 4 * FwdV2<128>::TILE, st, a);
-        else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP>), grid, block, 4 * FwdV2<64>::TILE, st, a);
+        constexpr int NW = SA_FWD_NW;
+        constexpr int BM = FwdV2<128, NW>::BM;
+        dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + BM - 1) / BM), block(64 * NW);
+        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, NW>), grid, block, (4 * FwdV2<128, NW>::TILE), st, a);
+        else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, NW>), grid, block, (4 * FwdV2<64, NW>::TILE), st, a);
         return;
     }
     dim3 grid((max_q + 127) / 128, a.Hq, a.nseg), block(256);

@@ -60,20 +60,6 @@ void gemm_tn(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, in
              int64_t K, bool beta, hipStream_t st, int full_blocks = -1, int split = 1, float* ws = nullptr);
 }  // namespace sa_launch
 
-// gemm_nt.hip: C[M, N] = A[M, K] B[N, K]^T (bf16, k-contiguous operands) with fused epilogues
-enum { EPI_STORE = 0, EPI_SWIGLU = 1, EPI_SWIGLU_BWD = 2 };
-struct NtEpi {
-    uint16_t* C; int64_t ldc;        // STORE: C; SWIGLU: z = [g | u] [M, 2F] (nullptr: not written); SWIGLU_BWD: dz [M, 2F]
-    uint16_t* H; int64_t ldh;        // SWIGLU: h = silu(g) u [M, F]
-    const uint16_t* Z; int64_t ldz;  // SWIGLU_BWD: z
-    int F;                           // SwiGLU intermediate features
-};
-namespace sa_launch {
-bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
-void gemm_nt(int epi, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
-               const NtEpi& ep, hipStream_t st);
-}  // namespace sa_launch
-
 // flash attention (bf16, head dim 32/64/128)
 struct FwdArgs {
     const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o; float* lse;

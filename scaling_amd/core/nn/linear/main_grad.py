@@ -57,7 +57,7 @@ from ...utils.debug_env import side_streams_enabled
 _GEN = [0]
 _WT_MODE = os.environ.get("SCALING_AMD_DGRAD_WT", "1")
 _WT_ENABLED = _WT_MODE != "0"
-# "all": also small weights (< 1M elements), so every tiling dgrad runs dY (W^T)^T on the NT GEMM path (forensics)
+# "all": also small weights (< 1M elements), so every dgrad runs dY (W^T)^T in the forward GEMM layout (tests)
 _WT_MIN_NUMEL = 0 if _WT_MODE == "all" else (1 << 20)
 
 

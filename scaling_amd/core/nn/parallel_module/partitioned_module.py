@@ -117,6 +117,11 @@ class PipePartitionedModule(torch.nn.Module):
                         )
                 self._layers.append(layer)
                 self._layer_devices.append(device)
+            # the last layer of a pipeline stage that feeds another stage hands its output to pipe p2p: layers that can
+            # leave part of their output pending (TransformerLayerIO.residual_branch) resolve it there, so a stage
+            # boundary moves (and a checkpoint saves) one tensor, not two
+            if c.end > c.start and c.end < len(self._layer_specs) and hasattr(self._layers[-1], "set_stage_output"):
+                self._layers[-1].set_stage_output(True)
 
     def _global_layer_indices(self) -> list[int]:
         return [li for c in self._pipe_partition_coordinates for li in range(c.start, c.end)]

@@ -13,9 +13,8 @@ _PRESETS: dict[str, dict[str, Any]] = {
     "llama2_70b": dict(hidden_size=8192, num_layers=80, num_attention_heads=64, kv_heads=8, ffn=28672),
     "llama_1b": dict(hidden_size=2048, num_layers=16, num_attention_heads=16, kv_heads=4, ffn=5632),
     "llama_tiny": dict(hidden_size=256, num_layers=2, num_attention_heads=4, kv_heads=2, ffn=688),
-    # llama_tiny with every GEMM dimension a multiple of 256 (ffn 768): every forward / dgrad / wgrad GEMM tiles onto
-    # the hand-written HIP kernels (SCALING_AMD_NT_GEMM=1, SCALING_AMD_DGRAD_WT=all), no vendor GEMM runs (race-check
-    # forensics: tests/test_gpu_rehearsal.py)
+    # llama_tiny with every GEMM dimension a multiple of 256 (ffn 768): every weight gradient tiles onto the
+    # hand-written HIP kernel and every dgrad onto the W^T cache (SCALING_AMD_DGRAD_WT=all; tests/test_gpu_e2e.py)
     "llama_tiny_r256": dict(hidden_size=256, num_layers=2, num_attention_heads=4, kv_heads=2, ffn=768),
 }
 

@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os
 import threading
 from typing import Callable, Any, Iterator, Optional
 
@@ -219,17 +218,6 @@ def _view(base: torch.Tensor, spec: tuple) -> torch.Tensor:
     return base.as_strided(shape, stride, base.storage_offset() + off)
 
 
-_DEBUG_SYNC_FA = os.environ.get("SCALING_AMD_DEBUG_SYNC_FA") == "1"
-
-
-def _probe_values(name: str, t: torch.Tensor) -> None:
-    from ..core.utils import grad_probe  # deferred: scaling_amd.core imports this module
-
-    grad_probe.record_values(name, t)
-_DEBUG_FA_TWICE = os.environ.get("SCALING_AMD_DEBUG_FA_TWICE") == "1"
-_DEBUG_UNFOLD_ROPE = os.environ.get("SCALING_AMD_DEBUG_UNFOLD_ROPE") == "1"
-
-
 def _probe_record(name: str, *tensors: Any) -> None:
     """Race-check forensics (``core/utils/grad_probe.record``; a no-op unless probing is on)."""
     from ..core.utils import grad_probe  # deferred: scaling_amd.core imports this module
@@ -258,62 +246,26 @@ class _RopeFlashAttn(torch.autograd.Function):
         return o
 
     @staticmethod
+    def bwd_into(ctx: Any, do: torch.Tensor, dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor) -> None:
+        """The attention backward written into the q/k/v slices (dq, dk, dv) of a dQKV buffer, the inverse rotation of
+        dq / dk folded into the dQ / dK epilogues.  (A separate method so race forensics can wrap it from outside the
+        production code: tools/attn_forensics.py.)"""
+        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
+        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
+        v = _view(base, specs[2])
+        ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
+                     local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
+
+    @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
         base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
         _probe_record("rope_flash.saved@bwd", base, q, k, o, lse, pos, cos, sin, cu_q)
         _probe_record("rope_flash.do", do)
-        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
+        specs = ctx.cfg[0]
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
-        v = _view(base, specs[2])
-        # the inverse rotation of dq / dk is folded into the attention backward's dQ / dK epilogues
-        sync = _DEBUG_SYNC_FA and base.is_cuda
-
-        def bwd_into(gq, gk, gv):
-            if _DEBUG_UNFOLD_ROPE:  # race forensics: plain dQ / dK epilogues, then the stand-alone inverse RoPE
-                ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, gq, gk, gv, p_drop,
-                             seed, local_heads)
-                gq.copy_(ext().rope(gq.contiguous(), cos, sin, pos, rot_dim, seq_len, interleaved, True))
-                gk.copy_(ext().rope(gk.contiguous(), cos, sin, pos, rot_dim, seq_len, interleaved, True))
-                return
-            ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, gq, gk, gv, p_drop, seed,
-                         local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
-
-        if sync:  # race forensics: nothing else may run beside the attention backward
-            torch.cuda.synchronize(base.device)
-        bwd_into(dq, dk, dv)
-        if sync:
-            torch.cuda.synchronize(base.device)
+        _RopeFlashAttn.bwd_into(ctx, do, dq, dk, dv)
         _probe_record("rope_flash.dbase", dbase)
-        if _DEBUG_FA_TWICE:  # race forensics: the same backward again, into a second buffer; record any difference
-            d2 = torch.empty_like(base)
-            q2, k2, v2 = (_view(d2, sp) for sp in specs)
-            bwd_into(q2, k2, v2)
-            d3 = torch.empty_like(base)  # a third time: which of the two is the odd one out
-            q3, k3, v3 = (_view(d3, sp) for sp in specs)
-            bwd_into(q3, k3, v3)
-            ne = d2 != dbase
-            f64 = dict(device=base.device, dtype=torch.float64)
-            first = torch.full((4,), -1.0, **f64)
-            nz = torch.nonzero(ne.reshape(-1))[:4].reshape(-1).double()
-            first[:nz.numel()] = nz
-            counts = torch.stack([(a != b).sum() for a, b in zip((q2, k2, v2), (dq, dk, dv))]).double()
-            # [total, dq, dk, dv, first 4 flat indices, row length, d3 == first, d3 == second, distinct rows,
-            #  max |difference|, up to 16 distinct columns (-1 padded)]
-            rows_ne, cols_ne = ne.reshape(ne.shape[0], -1).any(1), ne.reshape(ne.shape[0], -1).any(0)
-            cols = torch.full((16,), -1.0, **f64)
-            cz = torch.nonzero(cols_ne).reshape(-1)[:16].double()
-            cols[:cz.numel()] = cz
-            extra = torch.stack([torch.equal(d3, dbase) * torch.ones((), **f64), torch.equal(d3, d2) * torch.ones((), **f64),
-                                 rows_ne.sum().double(), (d2.float() - dbase.float()).abs().max().double()])
-            vals = torch.zeros(8, **f64)  # the first 4 differing elements: first run, then second run
-            ix = first[:nz.numel()].long()
-            vals[:nz.numel()] = dbase.reshape(-1)[ix].double()
-            vals[4:4 + nz.numel()] = d2.reshape(-1)[ix].double()
-            # [..., 16 columns, 8 values]
-            _probe_values("rope_flash.twice_mismatch", torch.cat([ne.sum().double().reshape(1), counts, first,
-                                                                   torch.tensor([float(dbase.shape[-1])], **f64), extra,
-                                                                   cols, vals]))
         return (dbase,) + (None,) * 17
 
 

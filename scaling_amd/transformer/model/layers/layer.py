@@ -28,6 +28,13 @@ _DEFER_RESIDUAL = os.environ.get("SCALING_AMD_DEFER_RESIDUAL", "1") != "0"
 _SP_OVERLAP = os.environ.get("SCALING_AMD_SP_OVERLAP", "1") != "0"
 
 
+def residual_defer_allowed(topology: Optional[Topology]) -> bool:
+    """Whether a layer may leave its MLP residual add pending under this topology's checkpointing: not when every
+    layer's input is a checkpoint boundary (every_layer*: the pending pair would be saved as two tensors)."""
+    ac = getattr(getattr(topology, "config", None), "activation_checkpointing_type", None)
+    return _DEFER_RESIDUAL and "every_layer" not in str(getattr(ac, "value", ac))
+
+
 class ZeroLayer(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return torch.zeros_like(x)
@@ -52,6 +59,10 @@ class TransformerLayer(TransformerLayerBaseIO):
         self.architecture_config = cfg
         self.topology = topology
         self.layer_index = layer_index
+        # whether this layer may hand its MLP residual add to the next layer (residual_branch): not across a pipeline
+        # stage boundary (set_stage_output) and not when every layer's input is a checkpoint boundary (the pending
+        # pair would be saved as two tensors instead of one)
+        self._defer_ok = residual_defer_allowed(topology)
         dev = _device(topology)
         bitfit = getattr(cfg.bitfit_bias_config, "name", None)
         dtype = cfg.precision.dtype
@@ -158,6 +169,11 @@ class TransformerLayer(TransformerLayerBaseIO):
     def mlp_block(self, hidden_state: torch.Tensor) -> torch.Tensor:
         return self._mlp_tail(hidden_state, self.post_attention_layernorm(hidden_state))
 
+    def set_stage_output(self, last_of_stage: bool) -> None:
+        """Called by the pipeline partitioner on the last layer of a stage that sends its output to the next stage."""
+        if last_of_stage:
+            self._defer_ok = False
+
     def forward(self, x: TransformerLayerIO) -> TransformerLayerIO:
         st = x.inference_settings
         assert x.cumulative_seq_lengths is not None
@@ -200,7 +216,7 @@ class TransformerLayer(TransformerLayerBaseIO):
                 act = fused(h, resid, self.post_attention_layernorm) if fused is not None else None
             if act is None:
                 resid, normed = self.post_attention_layernorm.forward_add(resid, h, gather=not sp)
-                if (_DEFER_RESIDUAL and not decode_step and not capture and not hasattr(self, "mlp_adapter_name")
+                if (self._defer_ok and not decode_step and not capture and not hasattr(self, "mlp_adapter_name")
                         and (self.dropout_mlp.p == 0.0 or not self.training)):
                     # leave resid + mlp(normed) to the next layer's add-norm (or the final norm)
                     branch = self.mlp(normed, sp_shard=True) if sp else self.mlp(normed)

@@ -102,7 +102,8 @@ def test_bench_sp_gather_overlap_gloo(extra):
 
 @pytest.mark.parametrize("preset,gpus,tp,pp,dp,acc,ac,sp,lora", [
     ("baseline3", 8, 2, 1, 4, 1, "disabled", True, False),
-    ("baseline4", 8, 2, 2, 2, 4, "every_layer_save_matmuls", True, False),
+    ("baseline4", 8, 2, 2, 2, 4, "every_layer", True, False),
+    ("baseline4_save_matmuls", 8, 2, 2, 2, 4, "every_layer_save_matmuls", True, False),
     ("baseline5", 8, 1, 1, 8, 1, "disabled", False, True),
     ("baseline3", 4, 2, 1, 2, 1, "disabled", True, False),
 ])
@@ -143,7 +144,7 @@ def test_bench_preset_runs_gloo():
     assert r.returncode == 0, r.stderr[-4000:]
     res = _json_lines(r.stdout)[0]
     assert res["config"]["preset"] == "baseline4"
-    assert res["config"]["parallelism"].startswith("tp2_pp2_dp1_zero1_ac-every_layer_save_matmuls_sp")
+    assert res["config"]["parallelism"].startswith("tp2_pp2_dp1_zero1_ac-every_layer_sp")
 
 
 def test_default_tp_comm_chunks():
@@ -164,7 +165,8 @@ def test_default_tp_comm_chunks():
     assert cfg["topology"]["tensor_parallel_comm_chunks"] == a.tp_comm_chunks >= 2
 
 
-@pytest.mark.parametrize("preset,ac", [("baseline3", None), ("baseline4", None), ("baseline4", "every_layer")])
+@pytest.mark.parametrize("preset,ac", [("baseline3", None), ("baseline4", None),
+                                       ("baseline4", "every_layer_save_matmuls")])
 def test_bench_shard_proxy_gloo(preset, ac):
     """``--shard-proxy``: one process runs rank 0's TP2 shard of the preset (one pipeline stage's layers) with stubbed
     collectives; the JSON says it is a per-rank proxy (not the headline), on one device, with the preset's layout
@@ -177,17 +179,19 @@ def test_bench_shard_proxy_gloo(preset, ac):
     assert res["metric"].startswith("per-rank proxy") and res["n_gpus"] == 1 and res["vs_baseline"] is None
     c = res["config"]
     assert c["shard_proxy"] == preset and c["tp"] == 2 and c["pp"] == 1 and c["dp"] == 1 and c["sequence_parallel"]
-    assert c["activation_checkpointing"] == (ac or ("every_layer_save_matmuls" if preset == "baseline4" else "disabled"))
+    assert c["activation_checkpointing"] == (ac or ("every_layer" if preset == "baseline4" else "disabled"))
     assert c["micro_batch"] == (4 if preset == "baseline4" else 8) and math.isfinite(c["loss"])
     assert c["proxy_8gpu_tokens_s_without_comm"] > 0
 
 
-@pytest.mark.parametrize("split,gpus,backend,want", [("1", 2, "gloo-gpu", ["0:0-127", "0:128-255"]),
-                                                     ("256", 4, "gloo-gpu", ["0:0-63", "0:64-127", "0:128-191", "0:192-255"]),
-                                                     ("1", 2, "gloo", [None, None]), ("0", 2, "gloo-gpu", [None, None])])
-def test_bench_launcher_cu_split(monkeypatch, split, gpus, backend, want):
-    """SCALING_AMD_REHEARSAL_CU_SPLIT gives each 1-GPU rehearsal rank a disjoint CU range (HSA_CU_MASK), only for the
-    GPU-sharing gloo-gpu backend."""
+@pytest.mark.parametrize("split,gpus,backend,ndev,want", [
+    ("1", 2, "gloo-gpu", 1, ["0:0-127", "0:128-255"]),
+    ("256", 4, "gloo-gpu", 1, ["0:0-63", "0:64-127", "0:128-191", "0:192-255"]),
+    ("1", 4, "gloo-gpu", 2, ["0:0-127", "1:0-127", "0:128-255", "1:128-255"]),  # ranks dealt over 2 visible devices
+    ("1", 2, "gloo", 1, [None, None]), ("0", 2, "gloo-gpu", 1, [None, None])])
+def test_bench_launcher_cu_split(monkeypatch, split, gpus, backend, ndev, want):
+    """SCALING_AMD_REHEARSAL_CU_SPLIT gives each rehearsal rank a disjoint CU range (HSA_CU_MASK) of the device it runs
+    on (rank % visible devices), only for the GPU-sharing gloo-gpu backend."""
     import argparse
 
     import bench
@@ -205,6 +209,7 @@ def test_bench_launcher_cu_split(monkeypatch, split, gpus, backend, want):
     monkeypatch.delenv("HSA_CU_MASK", raising=False)
     monkeypatch.setattr(bench.subprocess, "Popen", _Proc)
     monkeypatch.setattr(bench.signal, "signal", lambda *a: None)
+    monkeypatch.setattr(bench, "_visible_devices", lambda: ndev)
     a = argparse.Namespace(gpus=gpus, backend=backend, launch_timeout=10)
     assert bench._launch(a) == 0
     assert [e.get("HSA_CU_MASK") for e in envs] == want

@@ -583,63 +583,6 @@ def test_gemm_tn_ragged(M, N, K, accumulate):
     torch.testing.assert_close(out.float(), A.float().t() @ B.float(), atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 384), (1024, 512, 1024), (768, 1280, 11008 // 86 * 2),
-                                   (8192, 2304, 256), (4352, 4096, 384)])
-def test_gemm_nt(M, N, K):
-    """Forward / dgrad GEMM C = A B^T (64-deep staged kernel, csrc/kernels/gemm_nt.hip) against an fp32 reference,
-    with a strided (sliced) A and an asymmetric B.  The last two shapes have more tiles than CUs (288, 272), so
-    workgroups of the persistent kernel walk several tiles with the pipeline running on across them."""
-    torch.manual_seed(7)
-    A_full = torch.randn(M, K + 64, device=DEV, dtype=torch.bfloat16)
-    A = A_full[:, 64:]
-    B = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * torch.linspace(0.5, 1.5, K, device=DEV).to(torch.bfloat16)
-    C = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    assert ext().gemm_nt_ok(A, B)
-    ext().gemm_nt(A, B, C)
-    ref = A.float() @ B.float().t()
-    torch.testing.assert_close(C.float(), ref, atol=0.05 * math.sqrt(K / 64), rtol=1e-2)
-    assert not ext().gemm_nt_ok(A[:200], B)
-    assert not ext().gemm_nt_ok(A[:, : K - 64], B[:, : K - 64])
-    assert not ext().gemm_nt_ok(A[:, :128], B[:, :128])  # fewer than 4 k-stages
-
-
-@pytest.mark.parametrize("M,F,K", [(256, 256, 256), (512, 512, 256), (1024, 1024, 512), (8192, 2304, 256)])
-def test_gemm_nt_swiglu_epilogues(M, F, K):
-    """Fused SwiGLU epilogues of the NT GEMM: forward (z = x [W_g; W_u]^T, h = silu(g) u) and backward
-    (dz = swiglu_bwd(dY W_down, z)) are bit-identical to the unfused GEMM + SwiGLU kernels, and match an fp32
-    reference of the composite op."""
-    torch.manual_seed(11)
-    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(2 * F, K, device=DEV, dtype=torch.bfloat16) / math.sqrt(K)
-    z = torch.empty(M, 2 * F, device=DEV, dtype=torch.bfloat16)
-    h = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
-    assert ext().gemm_nt_swiglu_ok(x, w)
-    ext().gemm_nt_swiglu(x, w, z, h)
-    z_ref = torch.empty_like(z)
-    ext().gemm_nt(x, w, z_ref)
-    assert torch.equal(z, z_ref)
-    assert torch.equal(h, ext().swiglu_fwd(z_ref[:, :F], z_ref[:, F:]))
-    zf = x.float() @ w.float().t()
-    torch.testing.assert_close(h.float(), torch.nn.functional.silu(zf[:, :F]) * zf[:, F:], atol=3e-2, rtol=3e-2)
-    h2 = torch.empty_like(h)
-    ext().gemm_nt_swiglu(x, w, None, h2)  # inference form: z not written
-    assert torch.equal(h, h2)
-    H = 256
-    dy = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
-    wd = torch.randn(H, F, device=DEV, dtype=torch.bfloat16) / math.sqrt(F)
-    wdt = wd.t().contiguous()
-    dz = torch.empty_like(z)
-    ext().gemm_nt_swiglu_bwd(dy, wdt, z, dz)
-    dh = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
-    ext().gemm_nt(dy, wdt, dh)
-    (dz_ref,) = ext().swiglu_bwd(dh, z[:, :F], z[:, F:], True)
-    assert torch.equal(dz, dz_ref)
-    g, u = z[:, :F].float().requires_grad_(), z[:, F:].float().requires_grad_()
-    (torch.nn.functional.silu(g) * u).backward(dy.float() @ wd.float())
-    torch.testing.assert_close(dz[:, :F].float(), g.grad, atol=3e-2, rtol=3e-2)
-    torch.testing.assert_close(dz[:, F:].float(), u.grad, atol=3e-2, rtol=3e-2)
-
-
 # ---------------------------------------------------------------- masked softmax / activations / dropout
 from scaling_amd.ops import elementwise  # noqa: E402
 
@@ -1039,69 +982,24 @@ def test_rope_kv_append_bit_identical(interleaved, rot_frac):
 
 
 @pytest.mark.parametrize("T,H,F", [(512, 256, 512), (1024, 512, 768)])
-def test_swiglu_mlp_fused_node_matches_unfused(T, H, F, monkeypatch):
-    """ParallelSwiGLUMLP as ONE autograd node on the NT GEMM's SwiGLU epilogues (SCALING_AMD_NT_GEMM=1) gives the
-    output, input gradient and weight gradients of the unfused path (hipBLASLt GEMMs + SwiGLU kernels) to bf16
-    accuracy, and both match an fp32 reference."""
+def test_swiglu_mlp_matches_fp32_reference(T, H, F):
+    """ParallelSwiGLUMLP on the GPU path (fused gate/up GEMM, HIP SwiGLU kernels, HIP weight-gradient GEMM): output,
+    input gradient and weight gradients against an fp32 PyTorch reference of the same MLP."""
     from scaling_amd.core.nn.mlp import ParallelSwiGLUMLP
-    from scaling_amd.ops import gemm as gemm_ops
 
     torch.manual_seed(3)
     mlp = ParallelSwiGLUMLP(H, F / H, bias=False, device=torch.device(DEV), dtype=torch.bfloat16)
     x = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
     dy = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setattr(gemm_ops, "_NT_MODE", mode)
-        assert mlp._fused_eligible(x) == (mode == "1")
-        for p in mlp.parameters():
-            p.grad = None
-        xi = x.clone().requires_grad_(True)
-        y = mlp(xi)
-        y.backward(dy)
-        res[mode] = [y.float(), xi.grad.float()] + [p.grad.float() for p in (mlp.dense_in.weight,
-                                                                              mlp.siglu_weight.weight,
-                                                                              mlp.dense_out.weight)]
+    xi = x.clone().requires_grad_(True)
+    y = mlp(xi)
+    y.backward(dy)
+    got = [y.float(), xi.grad.float()] + [p.grad.float() for p in (mlp.dense_in.weight, mlp.siglu_weight.weight,
+                                                                     mlp.dense_out.weight)]
     xf = x.float().reshape(-1, H).requires_grad_(True)
     wg, wu, wd = (p.detach().float().requires_grad_(True) for p in (mlp.dense_in.weight, mlp.siglu_weight.weight,
                                                                    mlp.dense_out.weight))
     yf = (torch.nn.functional.silu(xf @ wg.t()) * (xf @ wu.t())) @ wd.t()
     yf.backward(dy.float().reshape(-1, H))
-    ref = [yf, xf.grad, wg.grad, wu.grad, wd.grad]
-    for a, b, r in zip(res["1"], res["0"], ref):
-        scale = r.abs().max().item()
-        assert (a.reshape(r.shape) - r).abs().max().item() < 0.03 * scale
-        assert (a - b).abs().max().item() < 0.03 * scale
-
-
-@pytest.mark.parametrize("T,H,F", [(512, 256, 512), (1024, 512, 768)])
-def test_swiglu_down_bwd_epilogue_matches_unfused(T, H, F, monkeypatch):
-    """The unfused forward with the SwiGLU backward on the down projection's dgrad epilogue (``_SwiGLUDown``,
-    SCALING_AMD_SWIGLU_BWD_NT=1) gives the output and every gradient of the all-unfused path to bf16 accuracy."""
-    from scaling_amd.core.nn import mlp as mlp_mod
-    from scaling_amd.ops import gemm as gemm_ops
-
-    torch.manual_seed(4)
-    monkeypatch.setattr(gemm_ops, "_NT_MODE", "0")  # keep the one-node fused MLP out of it
-    mlp = mlp_mod.ParallelSwiGLUMLP(H, F / H, bias=False, device=torch.device(DEV), dtype=torch.bfloat16)
-    x = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
-    dy = torch.randn(2, T // 2, H, device=DEV, dtype=torch.bfloat16)
-    calls = []
-    orig = mlp_mod._SwiGLUDown.apply
-    monkeypatch.setattr(mlp_mod._SwiGLUDown, "apply", lambda *a: calls.append(1) or orig(*a))
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setattr(gemm_ops, "_SWIGLU_BWD_MODE", mode)
-        for p in mlp.parameters():
-            p.grad = None
-        xi = x.clone().requires_grad_(True)
-        n = len(calls)
-        y = mlp(xi)
-        assert (len(calls) > n) == (mode == "1")
-        y.backward(dy)
-        res[mode] = [y.float(), xi.grad.float()] + [p.grad.float() for p in (mlp.dense_in.weight,
-                                                                              mlp.siglu_weight.weight,
-                                                                              mlp.dense_out.weight)]
-    assert torch.equal(res["1"][0], res["0"][0])  # same forward kernels
-    for a, b in zip(res["1"][1:], res["0"][1:]):
-        assert (a - b).abs().max().item() < 0.03 * b.abs().max().item()
+    for a, r in zip(got, [yf, xf.grad, wg.grad, wu.grad, wd.grad]):
+        assert (a.reshape(r.shape) - r).abs().max().item() < 0.03 * r.abs().max().item()

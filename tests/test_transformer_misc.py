@@ -190,3 +190,51 @@ def test_comm_volume_estimate_by_layout():
     e1 = comm_volume_estimate(hidden_size=h, num_layers=L, seq_len=s, micro_batch=8, grad_acc=1, tp=1, pp=1, dp=1,
                               params_per_rank=6_000_000_000)
     assert (e1["tp_bytes"], e1["pp_bytes"], e1["dp_bytes"]) == (0, 0, 0)
+
+
+class _StageProbe(torch.nn.Module):
+    """Layer stub recording whether the partitioner marked it as the output layer of a pipeline stage."""
+
+    def __init__(self) -> None:
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.zeros(1))
+        self.stage_output = False
+
+    def set_stage_output(self, last_of_stage: bool) -> None:
+        self.stage_output = last_of_stage
+
+
+def test_partitioner_marks_stage_output_layers():
+    """a transformer layer that leaves its MLP residual add pending (residual_branch) must not do so when its
+    output crosses a pipeline stage (p2p would move two tensors): the partitioner marks the last layer of every stage
+    that feeds another stage, and only those."""
+    from scaling_amd.core.nn.parallel_module.layer_spec import LayerSpec
+    from scaling_amd.core.nn.parallel_module.partitioned_module import PipePartitionedModule
+
+    specs = [LayerSpec(_StageProbe) for _ in range(7)]
+    m = PipePartitionedModule(specs, devices=["cpu", "cpu", "cpu"], pipe_partition_overwrite=[0, 3, 5, 7])
+    assert [layer.stage_output for layer in m._layers] == [False, False, True, False, True, False, False]
+
+
+@pytest.mark.parametrize("ac,defer", [("disabled", True), ("every_pipe_stage", True), ("every_layer", False),
+                                      ("every_layer_keep_attention", False), ("every_layer_save_matmuls", False)])
+def test_residual_defer_policy(ac, defer):
+    """The MLP residual add is handed to the next layer unless every layer input is a checkpoint boundary (the pending
+    pair would be saved as two tensors) or the layer is a stage output (set_stage_output)."""
+    from types import SimpleNamespace
+
+    from scaling_amd.core.topology.topology_config import ActivationCheckpointingType
+    from scaling_amd.models import llama_architecture
+    from scaling_amd.transformer.context.config import TransformerArchitectureConfig
+    from scaling_amd.transformer.model.layers import TransformerLayer
+
+    arch = TransformerArchitectureConfig(**llama_architecture("llama_tiny", sequence_length=32, vocab_size=64,
+                                                              precision="float32"))
+    from scaling_amd.transformer.model.layers.layer import _DEFER_RESIDUAL, residual_defer_allowed
+
+    topo = SimpleNamespace(config=SimpleNamespace(activation_checkpointing_type=ActivationCheckpointingType(ac)))
+    assert residual_defer_allowed(topo) == (defer and _DEFER_RESIDUAL)
+    real = TransformerLayer(arch, 0, None)
+    assert real._defer_ok is _DEFER_RESIDUAL
+    real.set_stage_output(True)
+    assert real._defer_ok is False

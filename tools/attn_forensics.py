@@ -1,0 +1,69 @@
+"""Race-check forensics for the fused RoPE + flash-attention backward, outside the production autograd node.
+
+Loaded into bench.py ranks with ``SCALING_AMD_DEBUG_HOOKS=tools/attn_forensics.py`` (``tools/race_trace.py`` passes it
+through); wraps ``ops.attention._RopeFlashAttn.bwd_into``:
+
+* ``ATTN_FORENSICS_SYNC=1``   device synchronisation right before and after every attention backward (nothing else
+  of the process may run beside it);
+* ``ATTN_FORENSICS_TWICE=1``  the same backward two more times into fresh buffers, with the differences recorded
+  through ``core/utils/grad_probe.record_values("rope_flash.twice_mismatch", ...)``:
+  [total, dq, dk, dv, first 4 flat indices, row length, third == first, third == second, distinct rows, max |diff|,
+  up to 16 distinct columns (-1 padded), first 4 differing values of the first run, then of the second].
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from scaling_amd.core.utils import grad_probe
+from scaling_amd.ops import attention
+
+_SYNC = os.environ.get("ATTN_FORENSICS_SYNC") == "1"
+_TWICE = os.environ.get("ATTN_FORENSICS_TWICE") == "1"
+_orig = attention._RopeFlashAttn.bwd_into
+
+
+def _mismatch(dbase: torch.Tensor, d2: torch.Tensor, d3: torch.Tensor, views1, views2) -> torch.Tensor:
+    f64 = dict(device=dbase.device, dtype=torch.float64)
+    ne = d2 != dbase
+    first = torch.full((4,), -1.0, **f64)
+    nz = torch.nonzero(ne.reshape(-1))[:4].reshape(-1).double()
+    first[:nz.numel()] = nz
+    counts = torch.stack([(a != b).sum() for a, b in zip(views2, views1)]).double()
+    rows_ne, cols_ne = ne.reshape(ne.shape[0], -1).any(1), ne.reshape(ne.shape[0], -1).any(0)
+    cols = torch.full((16,), -1.0, **f64)
+    cz = torch.nonzero(cols_ne).reshape(-1)[:16].double()
+    cols[:cz.numel()] = cz
+    extra = torch.stack([torch.equal(d3, dbase) * torch.ones((), **f64), torch.equal(d3, d2) * torch.ones((), **f64),
+                         rows_ne.sum().double(), (d2.float() - dbase.float()).abs().max().double()])
+    vals = torch.zeros(8, **f64)
+    ix = first[:nz.numel()].long()
+    vals[:nz.numel()] = dbase.reshape(-1)[ix].double()
+    vals[4:4 + nz.numel()] = d2.reshape(-1)[ix].double()
+    return torch.cat([ne.sum().double().reshape(1), counts, first, torch.tensor([float(dbase.shape[-1])], **f64), extra,
+                      cols, vals])
+
+
+def bwd_into(ctx, do, dq, dk, dv) -> None:
+    if _SYNC and do.is_cuda:
+        torch.cuda.synchronize(do.device)
+    _orig(ctx, do, dq, dk, dv)
+    if _SYNC and do.is_cuda:
+        torch.cuda.synchronize(do.device)
+    if not _TWICE:
+        return
+    base = ctx.saved_tensors[0]
+    specs = ctx.cfg[0]
+    dbase = dq.as_strided(base.shape, base.stride(), dq.storage_offset() - specs[0][2])
+    outs = []
+    for _ in range(2):
+        d = torch.empty_like(base)
+        views = [attention._view(d, sp) for sp in specs]
+        _orig(ctx, do, *views)
+        outs.append((d, views))
+    (d2, v2), (d3, _) = outs
+    grad_probe.record_values("rope_flash.twice_mismatch", _mismatch(dbase, d2, d3, (dq, dk, dv), v2))
+
+
+attention._RopeFlashAttn.bwd_into = staticmethod(bwd_into)

@@ -7,7 +7,6 @@
 #   bench      1-GPU bench.py (BENCH_ARGS)
 #   prof       rocprofv3 --kernel-trace --stats of 3 bench steps + per-category summary of the last step
 #   pmc        SQ/MFMA counters of every kernel of a 4-layer 7B-width step (PMC_PROG / PMC_ARGS: another program)
-#   gemm       tools/gemm_nt_bench.py (NT GEMM + SwiGLU epilogues vs hipBLASLt) and tools/gemm_nt_check.py
 #   attn       tools/attn_only.py (isolated attention at the 7B shape)
 #   decode     tools/decode_bench.py
 #   race       the multi- vs single-stream race check (tests/test_gpu_rehearsal.py -k race_check)
@@ -41,9 +40,6 @@ for step in "$@"; do
             GRBM_GUI_ACTIVE GRBM_COUNT -d "$R/gpurun_out/pmc_$TAG" -o a --output-format csv -- python3 $B \
             > "$R/gpurun_out/pmc_$TAG.log" 2>&1)
         $PY tools/pmc_csv_summary.py gpurun_out/pmc_$TAG > gpurun_out/pmc_$TAG.txt 2>&1 || true ;;
-    gemm)
-        $T 300 $PY tools/gemm_nt_check.py > gpurun_out/gemm_check_$TAG.log 2>&1
-        $T 400 $PY tools/gemm_nt_bench.py ${GEMM_ARGS:---rounds 3 --iters 8} > gpurun_out/gemm_$TAG.log 2>&1 ;;
     attn)
         $T 300 $PY tools/attn_only.py ${ATTN_ARGS:-} > gpurun_out/attn_$TAG.log 2>&1 ;;
     decode)
