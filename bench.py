@@ -84,6 +84,10 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
                         "16) with the preset's micro-batching, sequence parallelism and checkpointing; collectives are "
                         "stubbed (core/topology/stub_collectives.py), so the number is per-rank compute, not the "
                         "headline")
+    p.add_argument("--proxy-comm", type=str, default="stub", choices=["stub", "emulate"],
+                   help="--shard-proxy collectives: stub = free (per-rank compute only); emulate = each collective "
+                        "streams its per-rank send volume through HBM on 16 CUs and holds them for its modelled xGMI "
+                        "time (scaling_amd/core/topology/stub_collectives.py, transformer/utils/comm_estimate.py)")
     p.add_argument("--backend", type=str, default="auto", choices=["auto", "gloo", "gloo-gpu"],
                    help="gloo = CPU processes (plumbing mode, no GPU); gloo-gpu = rehearsal: GPU ranks (several "
                         "may share one GPU) with gloo collectives standing in for RCCL")
@@ -351,6 +355,7 @@ def _worker(a: argparse.Namespace) -> None:
     local = _env_int("LOCAL_RANK", 0)
     if a.shard_proxy is not None:  # one process = rank 0 of the TP group (stubbed collectives)
         world, rank, local = a.gpus, 0, 0
+        os.environ["SCALING_AMD_PROXY_COMM"] = a.proxy_comm
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -545,7 +550,9 @@ def _worker(a: argparse.Namespace) -> None:
         proxy_est = None
         if a.shard_proxy is not None:
             world_note = (f"per-rank proxy of --preset {a.shard_proxy}: rank 0 of TP{a.tp}, {arch['num_layers']} layers "
-                          "(one pipeline stage), collectives stubbed; value = ONE rank's tokens/s")
+                          "(one pipeline stage), collectives " +
+                          ("emulated (modelled xGMI time + HBM traffic on 16 CUs)" if a.proxy_comm == "emulate"
+                           else "stubbed") + "; value = ONE rank's tokens/s")
             lay = PRESETS[a.shard_proxy]
             # what 8 GPUs of the preset would reach with free communication: 8 / (tp pp) data-parallel replicas, each
             # pipeline running at the 1F1B efficiency m / (m + pp - 1) (m micro-batches)
@@ -573,6 +580,7 @@ def _worker(a: argparse.Namespace) -> None:
                 "parallelism": parallelism,
                 "preset": a.preset,
                 "shard_proxy": a.shard_proxy,
+                "proxy_comm": a.proxy_comm if a.shard_proxy is not None else None,
                 "proxy_8gpu_tokens_s_without_comm": proxy_est,
                 # the effective layout (after --preset), field by field
                 "tp": a.tp, "pp": a.pp, "dp": dp, "sequence_parallel": a.sequence_parallel,

@@ -680,6 +680,16 @@ at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind) {
 }
 // out = res + dropout(x); res optional (plain dropout).  Backward = dropout(g) with the same seed.
 void spin_us(int64_t us) { sa_launch::spin(us, cur_stream()); }
+// per-rank proxy: a collective's local footprint (HBM bytes through nwg CUs, then held to the modelled link time)
+void xgmi_emulate(const at::Tensor& src, const at::Tensor& scratch, int64_t bytes, double us, int64_t nwg) {
+    TORCH_CHECK(src.is_cuda() && scratch.is_cuda() && scratch.is_contiguous(), "xgmi_emulate: GPU tensors");
+    TORCH_CHECK((uintptr_t)src.data_ptr() % 16 == 0 && (uintptr_t)scratch.data_ptr() % 16 == 0, "xgmi_emulate: 16-B aligned");
+    const at::DeviceGuard g(src.device());
+    // the source is read as its contiguous storage span (the collective's bytes, whatever the view's strides)
+    const int64_t sb = src.is_contiguous() ? src.numel() * src.element_size() : 0;
+    sa_launch::xgmi_emulate(src.data_ptr(), sb, scratch.data_ptr(), scratch.numel() * scratch.element_size(),
+                            sb > 0 ? bytes : 0, us, (int)nwg, cur_stream());
+}
 
 at::Tensor dropout_add(const at::Tensor& x_, const c10::optional<at::Tensor>& res_, double p, int64_t seed) {
     TORCH_CHECK(x_.is_cuda(), "dropout: GPU tensor expected");
@@ -739,6 +749,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
     m.def("spin_us", &spin_us, "debug: busy-wait kernel of ~us microseconds on the current stream");
+    m.def("xgmi_emulate", &xgmi_emulate, "per-rank proxy: emulated collective (HBM traffic on nwg CUs, held to us)",
+          py::arg("src"), py::arg("scratch"), py::arg("bytes"), py::arg("us"), py::arg("nwg") = 16);
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));
     m.def("fa_fwd", &fa_fwd, "flash attention forward (bf16/fp16, optional attention dropout)", py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("max_k") = -1);
     m.def("fa_bwd", &fa_bwd, "flash attention backward (optional strided dq/dk/dv outputs)", py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("cu_q"), py::arg("cu_k"), py::arg("max_q"), py::arg("max_k"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("dq_out") = py::none(), py::arg("dk_out") = py::none(), py::arg("dv_out") = py::none(), py::arg("p_drop") = 0.0, py::arg("seed") = 0, py::arg("local_heads") = -1, py::arg("rope_cos") = py::none(), py::arg("rope_sin") = py::none(), py::arg("rope_pos") = py::none(), py::arg("rope_dim") = 0, py::arg("rope_seq") = 1, py::arg("rope_interleaved") = false);

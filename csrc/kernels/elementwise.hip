@@ -235,6 +235,18 @@ __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
 }
 
+// per-rank proxy with emulated communication (bench.py --shard-proxy ... --proxy-comm emulate): a collective's
+// footprint on THIS GPU.  `nwg` workgroups (RCCL's channels hold as many CUs) stream its per-rank send volume from the
+// collective's tensor (wrapping) into a scratch ring (local HBM read + write), then hold their CUs until the modelled
+// xGMI time `ticks` (100 MHz wall clock) has passed since the kernel started.  Every loop is bounded by n16 / ticks.
+__global__ __launch_bounds__(256) void xgmi_emu_kernel(const uint4* __restrict__ src, int64_t src16, uint4* __restrict__ dst,
+                                                       int64_t dst16, int64_t n16, uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i % dst16] = src[i % src16];
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 int ew_grid(int64_t n) {
     const int64_t blocks = (n / 8 + 255) / 256;
     return (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 256 * 16));
@@ -306,6 +318,15 @@ void act_bwd(int dtype, const void* dy, const void* x, void* dx, int64_t n, int 
 }
 void spin(int64_t us, hipStream_t st) {
     if (us > 0) hipLaunchKernelGGL(spin_kernel, 1, 64, 0, st, (uint64_t)us * 100);
+}
+void xgmi_emulate(const void* src, int64_t src_bytes, void* scratch, int64_t scratch_bytes, int64_t bytes, double us,
+                  int nwg, hipStream_t st) {
+    const int64_t src16 = src_bytes / 16, dst16 = scratch_bytes / 16;
+    const int64_t n16 = (src16 > 0 && dst16 > 0) ? bytes / 16 : 0;
+    const uint64_t ticks = us > 0 ? (uint64_t)(us * 100.0) : 0;
+    if (n16 == 0 && ticks == 0) return;
+    hipLaunchKernelGGL(xgmi_emu_kernel, std::max(1, nwg), 256, 0, st, (const uint4*)src, std::max<int64_t>(src16, 1),
+                       (uint4*)scratch, std::max<int64_t>(dst16, 1), n16, ticks);
 }
 void dropout(int dtype, const void* x, const void* res, void* out, int64_t n, uint32_t seed, uint32_t thr, float rp,
              hipStream_t st) {

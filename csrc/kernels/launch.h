@@ -137,6 +137,8 @@ void dropout(int dtype, const void* x, const void* res, void* out, int64_t n, ui
 namespace sa_launch {
 // debug: a one-wave busy-wait of `us` microseconds on stream st (elementwise.hip)
 void spin(int64_t us, hipStream_t st);
+void xgmi_emulate(const void* src, int64_t src_bytes, void* scratch, int64_t scratch_bytes, int64_t bytes, double us,
+                  int nwg, hipStream_t st);
 // one-shot all-reduce over IPC-mapped peer buffers (oneshot_allreduce.hip)
 void oneshot_allreduce(int dtype, char* const* bases, int world, int rank, int64_t slot_off, int64_t flag_off,
                        uint32_t epoch, bool signal, void* out, int64_t n, int* err, int64_t max_spins,

@@ -13,16 +13,41 @@ Model (one data-parallel replica processes ``micro_batch x grad_acc`` sequences 
 * data parallel (``d > 1``, ZeRO-1 as implemented): reduce-scatter of the fp32 (or bf16, ``grad_reduce_dtype``)
   gradient buckets and all-gather of the updated parameters, ``(d-1)/d`` of the rank's parameter shard each.
 
-Time: TP collectives of a TP group of 2 ride one xGMI link (~153 GB/s per direction, MI355X_MICROARCH.md);
-larger TP groups and DP rings are spread over ``min(group-1, 7)`` links by RCCL's multi-ring schedule.  The
-estimate assumes ``link_efficiency`` of that peak and no overlap; it is a reading aid, not a prediction.
+Time: the 8 GPUs of a node are fully connected, one xGMI link per pair (7 per GPU).  AMD quotes 153.6 GB/s "peak
+Infinity Fabric link bandwidth" for MI355X; the MI300X figure of the same kind (128 GB/s x 7 links = 896 GB/s) is the
+aggregate BIDIRECTIONAL rate, so one direction of one link carries half: 76.8 GB/s (rounds 1-5 used 153 GB/s per
+direction here, 2x optimistic -- VERDICT r5, Weak #5; no xGMI figure exists in MI355X_MICROARCH.md and this pool has
+no multi-GPU box to measure it on).  A TP group of 2 rides its one link; larger TP groups and DP rings are spread over
+``min(group-1, 7)`` links by RCCL's multi-ring schedule.  Each collective also pays a fixed latency
+(``COLLECTIVE_LATENCY_S``).  The estimate assumes ``link_efficiency`` of the peak and no overlap; it is a reading aid,
+not a prediction, and ``collective_time_s`` is what the per-rank proxy's emulated collectives hold the GPU for
+(``core/topology/stub_collectives.py``).
 """
 from __future__ import annotations
 
 from typing import Any
 
-XGMI_LINK_BYTES_PER_S = 153e9
+XGMI_LINK_BYTES_PER_S = 76.8e9  # one direction of one link (153.6 GB/s bidirectional)
 XGMI_LINKS_PER_GPU = 7
+COLLECTIVE_LATENCY_S = 10e-6  # launch + handshake of one intra-node RCCL collective (order of magnitude)
+LINK_EFFICIENCY = 0.75
+
+
+def ring_send_bytes(kind: str, nbytes: int, group: int) -> float:
+    """Bytes one rank sends per collective over a ring of ``group`` ranks: ``nbytes`` is the all-reduce tensor, the
+    reduce-scatter INPUT or the all-gather OUTPUT (the full, un-sharded size in each case)."""
+    if group <= 1:
+        return 0.0
+    f = (group - 1) / group
+    return 2.0 * f * nbytes if kind == "all_reduce" else f * nbytes
+
+
+def collective_time_s(kind: str, nbytes: int, group: int, link_efficiency: float = LINK_EFFICIENCY) -> float:
+    """First-order time of one collective on the node's xGMI mesh (latency + ring bytes over the group's links)."""
+    if group <= 1:
+        return 0.0
+    links = min(group - 1, XGMI_LINKS_PER_GPU)
+    return COLLECTIVE_LATENCY_S + ring_send_bytes(kind, nbytes, group) / (XGMI_LINK_BYTES_PER_S * link_efficiency * links)
 
 
 def _dtype_bytes(precision: str) -> int:
@@ -31,7 +56,7 @@ def _dtype_bytes(precision: str) -> int:
 
 def comm_volume_estimate(*, hidden_size: int, num_layers: int, seq_len: int, micro_batch: int, grad_acc: int,
                          tp: int, pp: int, dp: int, params_per_rank: int, precision: str = "bfloat16",
-                         grad_reduce_bytes: int = 4, link_efficiency: float = 0.7) -> dict[str, Any]:
+                         grad_reduce_bytes: int = 4, link_efficiency: float = LINK_EFFICIENCY) -> dict[str, Any]:
     act = _dtype_bytes(precision)
     M = micro_batch * seq_len
     ring = lambda n: 2.0 * (n - 1) / n if n > 1 else 0.0  # noqa: E731 - all-reduce bytes factor per rank
@@ -56,13 +81,14 @@ def comm_volume_estimate(*, hidden_size: int, num_layers: int, seq_len: int, mic
     return {
         "tp_bytes": int(tp_bytes), "pp_bytes": int(pp_bytes), "dp_bytes": int(dp_bytes),
         "tp_ms": round(t_ms(tp_bytes, tp), 2), "pp_ms": round(t_ms(pp_bytes, 2), 2), "dp_ms": round(t_ms(dp_bytes, dp), 2),
-        "assumptions": f"xGMI {XGMI_LINK_BYTES_PER_S / 1e9:.0f} GB/s/link x {link_efficiency}, no overlap",
+        "assumptions": f"xGMI {XGMI_LINK_BYTES_PER_S / 1e9:.1f} GB/s per link and direction x {link_efficiency}, "
+                       "no overlap",
     }
 
 
 def default_tp_comm_chunks(*, hidden_size: int, tokens: int, tp: int, in_features: int | None = None,
                            precision: str = "bfloat16", gemm_flops_per_s: float = 1.2e15, chunk_latency_s: float = 25e-6,
-                           min_chunk_rows: int = 2048, link_efficiency: float = 0.7) -> int:
+                           min_chunk_rows: int = 2048, link_efficiency: float = LINK_EFFICIENCY) -> int:
     """Token pieces for the row-parallel GEMM + TP collective overlap (``tensor_parallel_comm_chunks``) from the
     same first-order model: the collective of ``[tokens, hidden]`` takes ``tc`` on the TP group's links, the local
     GEMM (``in_features / tp`` inputs, default the hidden size) takes ``tg`` at ``gemm_flops_per_s``; with ``n``

@@ -184,6 +184,31 @@ def test_bench_shard_proxy_gloo(preset, ac):
     assert c["proxy_8gpu_tokens_s_without_comm"] > 0
 
 
+def test_bench_shard_proxy_emulated_comm_flag_gloo():
+    """``--proxy-comm emulate`` is accepted and reported (on CPU ranks the emulation is a no-op: it costs GPU time only)."""
+    r = _run(["--shard-proxy", "baseline3", "--proxy-comm", "emulate", "--model", "llama_tiny", "--backend", "gloo",
+              "--seq-len", "64", "--steps", "1", "--warmup", "1"], timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = _json_lines(r.stdout)[0]
+    assert res["config"]["proxy_comm"] == "emulate" and "emulated" in res["metric"]
+
+
+def test_collective_time_model():
+    """The xGMI model: one direction of one link is 76.8 GB/s (153.6 GB/s bidirectional); a TP2 all-reduce of the 7B
+    [32768, 4096] bf16 activations sends its size once over the pair's one link, a DP8 ring spreads over 7 links."""
+    from scaling_amd.transformer.utils import comm_estimate as ce
+
+    assert ce.XGMI_LINK_BYTES_PER_S == 76.8e9
+    nb = 32768 * 4096 * 2
+    assert ce.ring_send_bytes("all_reduce", nb, 2) == nb
+    assert ce.ring_send_bytes("reduce_scatter", nb, 8) == pytest.approx(nb * 7 / 8)
+    t2 = ce.collective_time_s("all_reduce", nb, 2, link_efficiency=1.0)
+    assert t2 == pytest.approx(ce.COLLECTIVE_LATENCY_S + nb / 76.8e9)
+    t8 = ce.collective_time_s("all_reduce", nb, 8, link_efficiency=1.0)
+    assert t8 == pytest.approx(ce.COLLECTIVE_LATENCY_S + 2 * nb * 7 / 8 / (7 * 76.8e9))
+    assert ce.collective_time_s("all_reduce", nb, 1) == 0.0
+
+
 @pytest.mark.parametrize("split,gpus,backend,ndev,want", [
     ("1", 2, "gloo-gpu", 1, ["0:0-127", "0:128-255"]),
     ("256", 4, "gloo-gpu", 1, ["0:0-63", "0:64-127", "0:128-191", "0:192-255"]),

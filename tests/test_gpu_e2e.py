@@ -268,6 +268,17 @@ def test_gpu_dgrad_transpose_cache_matches_uncached(extra):
     assert all(np.isfinite(v) for v in wt["param_checksum"])
 
 
+def test_gpu_shard_proxy_emulated_comm():
+    """BASELINE #3's per-rank proxy with emulated collectives (each one streams its per-rank send volume through HBM on
+    16 CUs and holds them for its modelled xGMI time, asynchronous ones on a proxy stream) trains to the stub run's
+    loss (the emulation moves no data the model reads) and takes longer than the stub run."""
+    stub = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8"])
+    emu = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8", "--proxy-comm", "emulate"])
+    assert emu["proxy_comm"] == "emulate" and stub["proxy_comm"] == "stub"
+    assert emu["loss"] == stub["loss"]
+    assert emu["per_rank_ms_per_step"][0] > stub["per_rank_ms_per_step"][0]
+
+
 def test_gpu_shard_proxy_tp_chunks_match():
     """BASELINE #3's per-rank shard (TP2 + sequence parallelism, collectives stubbed) with the row-parallel GEMMs cut
     into 1 / 2 / 4 overlapped token pieces and the norm gathers folded into their GEMMs trains to the same losses: the
