@@ -99,7 +99,33 @@ def _args(argv: Optional[list[str]] = None) -> argparse.Namespace:
     p.add_argument("--profile-json", type=str, default=None, help="write per-step times to this file")
     p.add_argument("--launch-timeout", type=float, default=3000.0, help="launcher: kill all ranks after this many s")
     argv = sys.argv[1:] if argv is None else argv
-    return apply_shard_proxy(apply_preset(p.parse_args(argv), argv), argv)
+    return apply_example(apply_shard_proxy(apply_preset(p.parse_args(argv), argv), argv), argv)
+
+
+# BASELINE.json config 2: "examples/transformer_example config.yml small GPT, TP=1 PP=1 DP=1 bf16 on one MI355X"
+EXAMPLE_CONFIG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "examples", "transformer_example", "config.yml")
+
+
+def example_config() -> dict[str, Any]:
+    """The transformer example's config (examples/transformer_example/config.yml) as a dict."""
+    from scaling_amd.transformer import TransformerConfig
+
+    return TransformerConfig.from_yaml(EXAMPLE_CONFIG).as_dict()
+
+
+def apply_example(a: argparse.Namespace, argv: Optional[list[str]] = None) -> argparse.Namespace:
+    """``--model transformer_example``: the example's model, micro-batching and sequence length (explicit flags win)."""
+    if a.model != "transformer_example":
+        return a
+    given = _explicit_flags(argv or [])
+    t = example_config()["topology"]
+    if "micro_batch" not in given:
+        a.micro_batch = t["micro_batch_size"]
+    if "grad_acc" not in given:
+        a.grad_acc = t["gradient_accumulation_steps"]
+    if "seq_len" not in given:
+        a.seq_len = example_config()["transformer_architecture"]["sequence_length"]
+    return a
 
 
 # BASELINE.json configs 3-5 (the 8-GPU layouts; any N the layout divides).  Values override the corresponding flags.
@@ -293,7 +319,11 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
     from scaling_amd.models import llama_architecture
 
     dp = world // (a.tp * a.pp)
-    arch = llama_architecture(a.model, sequence_length=a.seq_len, precision=a.precision)
+    ex = example_config() if a.model == "transformer_example" else None
+    if ex is not None:  # the example's architecture, optimizer and schedule as written (BASELINE #2)
+        arch = dict(ex["transformer_architecture"], sequence_length=a.seq_len)
+    else:
+        arch = llama_architecture(a.model, sequence_length=a.seq_len, precision=a.precision)
     if a.num_layers is not None:
         arch["num_layers"] = a.num_layers
     training: dict[str, Any] = {"weight_decay": 0.1}
@@ -318,13 +348,19 @@ def _config_dict(a: argparse.Namespace, world: int, rank: int, local: int) -> di
         topo["gloo_on_gpu"] = a.backend == "gloo-gpu"
     if a.shard_proxy is not None:
         topo["backend"] = "fake"
+    optim = {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0}
+    lrs = {"learning_rate": 3e-4, "learning_rate_minimum": 3e-5, "learning_rate_decay_style": "cosine",
+           "learning_rate_warmup_steps": 2, "learning_rate_decay_iters": 1000}
+    if ex is not None:
+        optim = {k: ex["optimizer"][k] for k in ("beta1", "beta2", "eps", "gradient_clipping", "allreduce_bucket_size")}
+        lrs = dict(ex["learning_rate_scheduler"])
+        training = dict(weight_decay=ex["training"]["weight_decay"], **{k: v for k, v in training.items()
+                                                                        if k != "weight_decay"})
     return {
         "topology": topo,
-        "optimizer": {"beta1": 0.9, "beta2": 0.95, "eps": 1e-8, "gradient_clipping": 1.0, "zero": bool(a.zero),
-                      "overlap_optimizer_step": bool(a.overlap_step), "lazy_grad_zeroing": bool(a.lazy_zero)},
-        "learning_rate_scheduler": {"learning_rate": 3e-4, "learning_rate_minimum": 3e-5,
-                                    "learning_rate_decay_style": "cosine", "learning_rate_warmup_steps": 2,
-                                    "learning_rate_decay_iters": 1000},
+        "optimizer": {**optim, "zero": bool(a.zero), "overlap_optimizer_step": bool(a.overlap_step),
+                      "lazy_grad_zeroing": bool(a.lazy_zero)},
+        "learning_rate_scheduler": lrs,
         "training": training,
         "trainer": {"seed": 42, "train_iterations": a.warmup + a.steps},
         "logger": {"log_level": "warning"},
@@ -558,7 +594,9 @@ def _worker(a: argparse.Namespace) -> None:
             # pipeline running at the 1F1B efficiency m / (m + pp - 1) (m micro-batches)
             proxy_est = (tokens / sec) * 8 / (lay["tp"] * lay["pp"]) * a.grad_acc / (a.grad_acc + lay["pp"] - 1)
         res = {
-            "metric": METRIC if a.shard_proxy is None else "per-rank proxy tokens/s (NOT the headline): " + world_note,
+            "metric": ("per-rank proxy tokens/s (NOT the headline): " + world_note if a.shard_proxy is not None else
+                       "tokens/sec examples/transformer_example small GPT bf16 (BASELINE #2)"
+                       if a.model == "transformer_example" else METRIC),
             "value": tokens / sec,
             "unit": "tokens/s",
             "n_gpus": world if a.shard_proxy is None else 1,
@@ -568,13 +606,17 @@ def _worker(a: argparse.Namespace) -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (tokens / sec) / (REFERENCE_TOK_S_1GPU * world) if headline and not a.lora else None,
-            "baseline": "unmodified reference on MI355X (torch attention, best micro-batch 2 x acc 4): "
-                        f"{REFERENCE_TOK_S_1GPU:.0f} tok/s per GPU x n_gpus (BASELINE.md)",
+            "baseline": ("unmodified reference on MI355X (torch attention, best micro-batch 2 x acc 4): "
+                         f"{REFERENCE_TOK_S_1GPU:.0f} tok/s per GPU x n_gpus (BASELINE.md)" if headline else None),
             "dtype": "bf16" if a.precision == "bfloat16" else "fp32",
             "data": "synthetic (random token ids, random-init weights)",
             "config": {
                 "model": ("Llama-2-7B-shape (h4096 L32 heads32 kv8 GQA, SwiGLU 11008, RoPE, RMSNorm, V32000)"
-                          if headline else f"{a.model} layers={arch['num_layers']} seq={a.seq_len} (NOT headline)"),
+                          if headline else
+                          "examples/transformer_example config.yml small GPT (BASELINE #2, NOT the headline): "
+                          f"h{arch['hidden_size']} L{arch['num_layers']} heads{arch['num_attention_heads']} "
+                          f"V{arch['vocab_size']} seq {a.seq_len}" if a.model == "transformer_example" else
+                          f"{a.model} layers={arch['num_layers']} seq={a.seq_len} (NOT headline)"),
                 "global_batch": gbs,
                 "seq_len": a.seq_len,
                 "parallelism": parallelism,

@@ -4,6 +4,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -680,6 +681,32 @@ at::Tensor act_bwd(const at::Tensor& dy_, const at::Tensor& x_, int64_t kind) {
 }
 // out = res + dropout(x); res optional (plain dropout).  Backward = dropout(g) with the same seed.
 void spin_us(int64_t us) { sa_launch::spin(us, cur_stream()); }
+// ---- stream gates (asynchronous rehearsal collectives, core/topology/gloo_gpu.py): a stream waits in the command
+// processor (hipStreamWaitValue32, no CU spins) until the host writes a generation number into a flag word.
+// kind 0: hipMallocSignalMemory words; kind 1: coherent pinned host memory.  Returns the base address.
+int64_t gate_flags_alloc(int64_t n, int64_t kind) {
+    void* p = nullptr;
+    const size_t bytes = (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t);
+    if (kind == 0) {
+        TORCH_CHECK(hipExtMallocWithFlags(&p, bytes, hipMallocSignalMemory) == hipSuccess, "gate: signal memory");
+    } else {
+        TORCH_CHECK(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess, "gate: pinned memory");
+    }
+    std::memset(p, 0, bytes);
+    return (int64_t)(uintptr_t)p;
+}
+void gate_flag_write(int64_t base, int64_t idx, int64_t value) {
+    std::atomic_thread_fence(std::memory_order_seq_cst);  // every host write before (the results) lands first
+    __atomic_store_n(reinterpret_cast<uint32_t*>((uintptr_t)base) + idx, (uint32_t)value, __ATOMIC_SEQ_CST);
+}
+int64_t gate_flag_read(int64_t base, int64_t idx) {
+    return __atomic_load_n(reinterpret_cast<uint32_t*>((uintptr_t)base) + idx, __ATOMIC_SEQ_CST);
+}
+void gate_stream_wait(int64_t base, int64_t idx, int64_t value) {
+    void* p = reinterpret_cast<uint32_t*>((uintptr_t)base) + idx;
+    TORCH_CHECK(hipStreamWaitValue32(cur_stream(), p, (uint32_t)value, hipStreamWaitValueGte, 0xFFFFFFFFu) == hipSuccess,
+                "gate: hipStreamWaitValue32 failed");
+}
 // per-rank proxy: a collective's local footprint (HBM bytes through nwg CUs, then held to the modelled link time)
 void xgmi_emulate(const at::Tensor& src, const at::Tensor& scratch, int64_t bytes, double us, int64_t nwg) {
     TORCH_CHECK(src.is_cuda() && scratch.is_cuda() && scratch.is_contiguous(), "xgmi_emulate: GPU tensors");
@@ -749,6 +776,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
     m.def("spin_us", &spin_us, "debug: busy-wait kernel of ~us microseconds on the current stream");
+    m.def("gate_flags_alloc", &gate_flags_alloc, "stream gates: n flag words (kind 0 signal memory, 1 pinned host)");
+    m.def("gate_flag_write", &gate_flag_write, "stream gates: host store of a flag word (after a full fence)");
+    m.def("gate_flag_read", &gate_flag_read, "stream gates: host load of a flag word");
+    m.def("gate_stream_wait", &gate_stream_wait, "stream gates: the current stream waits until flag[idx] >= value");
     m.def("xgmi_emulate", &xgmi_emulate, "per-rank proxy: emulated collective (HBM traffic on nwg CUs, held to us)",
           py::arg("src"), py::arg("scratch"), py::arg("bytes"), py::arg("us"), py::arg("nwg") = 16);
     m.def("dropout_add", &dropout_add, "residual + dropout(x) with a hashed keep mask", py::arg("x"), py::arg("res"), py::arg("p"), py::arg("seed"));

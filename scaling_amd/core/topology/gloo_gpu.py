@@ -8,16 +8,34 @@ runs even with every side stream folded onto the compute stream (``profiles/race
 fresh box differs, the warm reruns agree, independent of which side stream is folded).
 
 ``install()`` wraps the ``torch.distributed`` collectives this framework calls so that GPU tensors travel through
-host copies: the device-to-host copy of every input is ordered after the current stream's work (and synchronous),
-gloo runs on host tensors, and the results are copied back on the current stream -- exactly the stream semantics
-RCCL has, so the rehearsal's multi- vs single-stream comparison again tests this framework's own stream / event
-ordering.  Sums over 3+ ranks are done in rank order (``_ordered_sum``): gloo's own order follows message arrival.  ``async_op=True`` calls complete before returning (their work handle's ``wait`` is a no-op).  Only the
-rehearsal installs this; with RCCL (``nccl``) or CPU gloo nothing is wrapped.  The same for pipeline p2p is
-``communicator._HostStagedWork``.
+host copies, gloo runs on host tensors and sums over 3+ ranks are done in rank order (``_ordered_sum``: gloo's own
+order follows message arrival).  Two modes:
+
+* synchronous (default): the device-to-host copy of every input is ordered after the current stream's work and waited
+  for, gloo runs, the results are copied back on the current stream; ``async_op=True`` calls complete before
+  returning.  Stream order is RCCL's, but the collective has READ its input and its result is on the way before the
+  call returns -- so a tensor freed or reused too early, or a consumer stream that does not wait for the
+  communication stream, stays invisible.
+* asynchronous (``SCALING_AMD_REHEARSAL_ASYNC=1``): RCCL's lifetimes.  The call only ENQUEUES, on the
+  current stream (``async_op=True``: on a side stream that first waits for the current one, the work handle's ``wait``
+  makes the waiting stream wait for it, and the handle keeps the tensors alive, as ProcessGroupNCCL does): the input's
+  device-to-host copy into pinned memory, a stream gate (``hipStreamWaitValue32`` on a flag word: the stream holds in
+  the command processor, no CU spins), and the host-to-device copy of the result.  One worker thread per process runs
+  every gloo call in program order (also the CPU-tensor and object collectives, so both ranks issue gloo work in the same
+  order): it waits until the stream has copied the input out, runs gloo on the host copies, writes the result, and
+  opens the gate.  So the input is read when the STREAM gets there, long after the call returned, and the output lands
+  when the peers are done -- a missing ``record_stream`` / early free / missing stream wait in this framework changes
+  the result, which the race check's multi- vs single-stream comparison then shows.  Pipeline p2p is refused in this
+  mode (its host staging, ``communicator._HostStagedWork``, is synchronous).
+
+Only the rehearsal installs this; with RCCL (``nccl``) or CPU gloo nothing is wrapped.
 """
 from __future__ import annotations
 
 import functools
+import os
+import queue
+import threading
 from typing import Any, Callable, Optional
 
 import torch
@@ -25,6 +43,7 @@ import torch.distributed as dist
 
 _installed = False
 _orig: dict[str, Callable[..., Any]] = {}
+_ASYNC = os.environ.get("SCALING_AMD_REHEARSAL_ASYNC", "0") == "1"
 
 
 class _Done:
@@ -68,17 +87,184 @@ def _is_sum(op: Any) -> bool:
     return op is None or op == dist.ReduceOp.SUM
 
 
+def _op(op: Any) -> Any:
+    return op if op is not None else dist.ReduceOp.SUM
+
+
+# ------------------------------------------------------------------------------------------ host-side algorithms
+# Each takes host copies of the GPU inputs and returns the host result to copy into the GPU output (both modes).
+def _h_all_reduce(h: torch.Tensor, op: Any, group: Any) -> torch.Tensor:
+    red = _ordered_sum(h, group) if _is_sum(op) else None
+    if red is None:
+        _orig["all_reduce"](h, _op(op), group)
+        red = h
+    return red
+
+
+def _h_reduce_scatter(hi: torch.Tensor, out_shape: torch.Size, out_dtype: torch.dtype, op: Any, group: Any) -> torch.Tensor:
+    red = _ordered_sum(hi, group) if _is_sum(op) else None
+    if red is None:
+        ho = torch.empty(out_shape, dtype=out_dtype)
+        _orig["reduce_scatter_tensor"](ho, hi, _op(op), group)
+        return ho
+    r, n = dist.get_rank(group), int(torch.Size(out_shape).numel())
+    return red.reshape(-1)[r * n:(r + 1) * n].reshape(out_shape)
+
+
+# ------------------------------------------------------------------------------------------ asynchronous mode
+class _Worker:
+    """Runs every gloo call of this process, in submission (= program) order, on one thread."""
+
+    def __init__(self) -> None:
+        self.q: "queue.Queue[Optional[tuple[Callable[[], Any], Any]]]" = queue.Queue()
+        self.error: Optional[BaseException] = None
+        self.t = threading.Thread(target=self._loop, name="gloo-gpu-async", daemon=True)
+        self.t.start()
+
+    def _loop(self) -> None:
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            fn, fut = item
+            try:
+                fut["value"] = fn()
+            except BaseException as e:  # noqa: BLE001 - re-raised on the caller's next call
+                fut["error"] = e
+                self.error = self.error or e
+            finally:
+                fut["done"].set()
+
+    def submit(self, fn: Callable[[], Any]) -> dict[str, Any]:
+        if self.error is not None:
+            raise RuntimeError("asynchronous rehearsal collective failed") from self.error
+        fut: dict[str, Any] = {"done": threading.Event()}
+        self.q.put((fn, fut))
+        return fut
+
+    def call(self, fn: Callable[[], Any]) -> Any:
+        fut = self.submit(fn)
+        fut["done"].wait()
+        if "error" in fut:
+            raise fut["error"]
+        return fut.get("value")
+
+    def drain(self) -> None:
+        self.call(lambda: None)
+
+
+class _Gates:
+    """A ring of flag words; each use of a word waits for the next generation number."""
+
+    def __init__(self, n: int = 1 << 14) -> None:
+        from ...ops._ext import ext
+
+        kind = int(os.environ.get("SCALING_AMD_REHEARSAL_GATE_KIND", "1"))
+        self.base = ext().gate_flags_alloc(n, kind)
+        self.n, self.i = n, 0
+        self.gen = [0] * n
+
+    def take(self) -> tuple[int, int]:
+        i = self.i % self.n
+        self.i += 1
+        self.gen[i] += 1
+        return i, self.gen[i]
+
+
+class _AsyncWork:
+    """Handle of an ``async_op=True`` collective: ``wait`` makes the current stream wait for its side stream."""
+
+    def __init__(self, ev: Any, keep: tuple) -> None:
+        self.ev, self.keep = ev, keep
+
+    def wait(self, timeout: Any = None) -> bool:
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+    def is_completed(self) -> bool:
+        return bool(self.ev.query())
+
+
+_state: dict[str, Any] = {}
+
+
+def _worker() -> _Worker:
+    if "worker" not in _state:
+        _state["worker"] = _Worker()
+    return _state["worker"]
+
+
+def _side_stream(dev: torch.device) -> Any:
+    key = ("side", dev.index)
+    if key not in _state:
+        _state[key] = torch.cuda.Stream(device=dev)
+    return _state[key]
+
+
+def _retire_pinned() -> None:
+    """Drops the pinned staging buffers whose host-to-device copy has completed."""
+    live = _state.setdefault("pinned", [])
+    live[:] = [(ev, bufs) for ev, bufs in live if not ev.query()]
+
+
+def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[torch.Tensor], torch.Tensor],
+             async_op: bool) -> Any:
+    """RCCL-like collective: input copy-out, gate and result copy-in enqueued on the stream; gloo in the worker."""
+    from ...ops._ext import ext
+
+    if "gates" not in _state:
+        _state["gates"] = _Gates()
+    gates = _state["gates"]
+    _retire_pinned()
+    cur = torch.cuda.current_stream(gpu_out.device)
+    st = _side_stream(gpu_out.device) if async_op else cur
+    if async_op:
+        st.wait_stream(cur)
+    h_in = torch.empty(gpu_in.shape, dtype=gpu_in.dtype, pin_memory=True)
+    h_out = torch.empty(gpu_out.shape, dtype=gpu_out.dtype, pin_memory=True)
+    idx, gen = gates.take()
+    with torch.cuda.stream(st):
+        h_in.copy_(gpu_in, non_blocking=True)  # read when the stream gets here
+        e_in = torch.cuda.Event()
+        e_in.record(st)
+        ext().gate_stream_wait(gates.base, idx, gen)
+        gpu_out.copy_(h_out, non_blocking=True)  # written once the peers are done
+        e_out = torch.cuda.Event()
+        e_out.record(st)
+    _state.setdefault("pinned", []).append((e_out, (h_in, h_out)))
+
+    def job() -> None:
+        try:
+            e_in.synchronize()
+            res = host_fn(h_in)
+            if res is not h_out:
+                h_out.copy_(res.reshape(h_out.shape))
+        finally:  # always open the gate: a failed collective must not leave the stream waiting (the error is raised)
+            ext().gate_flag_write(gates.base, idx, gen)
+
+    _worker().submit(job)
+    if async_op:
+        gpu_in.record_stream(st)
+        gpu_out.record_stream(st)
+        return _AsyncWork(e_out, (gpu_in, gpu_out))
+    return None
+
+
+def _host_call(fn: Callable[[], Any]) -> Any:
+    """A gloo call on host tensors / objects: through the worker in asynchronous mode (global order), else direct."""
+    return _worker().call(fn) if _ASYNC and _installed else fn()
+
+
+# ------------------------------------------------------------------------------------------ wrappers
 def _wrap_all_reduce(orig: Callable[..., Any]) -> Callable[..., Any]:
     @functools.wraps(orig)
     def fn(tensor: torch.Tensor, op: Any = None, group: Any = None, async_op: bool = False) -> Any:
         if not _cuda(tensor):
-            return orig(tensor, op if op is not None else dist.ReduceOp.SUM, group, async_op)
+            return _host_call(lambda: orig(tensor, _op(op), group, async_op))
+        if _ASYNC and tensor.is_contiguous():
+            return _enqueue(tensor, tensor, lambda h: _h_all_reduce(h, op, group), async_op)
         h = _host(tensor)
-        red = _ordered_sum(h, group) if _is_sum(op) else None
-        if red is None:
-            orig(h, op if op is not None else dist.ReduceOp.SUM, group)
-            red = h
-        tensor.copy_(red)
+        tensor.copy_(_host_call(lambda: _h_all_reduce(h, op, group)))
         return _Done() if async_op else None
 
     return fn
@@ -88,10 +274,16 @@ def _wrap_broadcast(orig: Callable[..., Any]) -> Callable[..., Any]:
     @functools.wraps(orig)
     def fn(tensor: torch.Tensor, *args: Any, async_op: bool = False, **kwargs: Any) -> Any:
         if not _cuda(tensor):
-            return orig(tensor, *args, async_op=async_op, **kwargs)
+            return _host_call(lambda: orig(tensor, *args, async_op=async_op, **kwargs))
+
+        def host(h: torch.Tensor) -> torch.Tensor:
+            orig(h, *args, **kwargs)
+            return h
+
+        if _ASYNC and tensor.is_contiguous():
+            return _enqueue(tensor, tensor, host, async_op)
         h = _host(tensor)
-        orig(h, *args, **kwargs)
-        tensor.copy_(h)
+        tensor.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
 
     return fn
@@ -102,16 +294,12 @@ def _wrap_reduce_scatter(orig: Callable[..., Any]) -> Callable[..., Any]:
     def fn(output: torch.Tensor, input: torch.Tensor, op: Any = None, group: Any = None,
            async_op: bool = False) -> Any:
         if not (_cuda(output) or _cuda(input)):
-            return orig(output, input, op if op is not None else dist.ReduceOp.SUM, group, async_op)
-        hi = _host(input)
-        red = _ordered_sum(hi, group) if _is_sum(op) else None
-        if red is None:
-            ho = torch.empty(output.shape, dtype=output.dtype)
-            orig(ho, hi, op if op is not None else dist.ReduceOp.SUM, group)
-        else:
-            r, n = dist.get_rank(group), output.numel()
-            ho = red.reshape(-1)[r * n:(r + 1) * n].reshape(output.shape)
-        output.copy_(ho)
+            return _host_call(lambda: orig(output, input, _op(op), group, async_op))
+        host = lambda h: _h_reduce_scatter(h, output.shape, output.dtype, op, group)  # noqa: E731
+        if _ASYNC and _cuda(output) and _cuda(input) and input.is_contiguous() and output.is_contiguous():
+            return _enqueue(input, output, host, async_op)
+        h = _host(input)
+        output.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
 
     return fn
@@ -121,30 +309,53 @@ def _wrap_all_gather_into(orig: Callable[..., Any]) -> Callable[..., Any]:
     @functools.wraps(orig)
     def fn(output: torch.Tensor, input: torch.Tensor, *args: Any, async_op: bool = False, **kwargs: Any) -> Any:
         if not (_cuda(output) or _cuda(input)):
-            return orig(output, input, *args, async_op=async_op, **kwargs)
-        ho = torch.empty(output.shape, dtype=output.dtype)
-        orig(ho, _host(input), *args, **kwargs)
-        output.copy_(ho)
+            return _host_call(lambda: orig(output, input, *args, async_op=async_op, **kwargs))
+
+        def host(h: torch.Tensor) -> torch.Tensor:
+            ho = torch.empty(output.shape, dtype=output.dtype)
+            orig(ho, h, *args, **kwargs)
+            return ho
+
+        if _ASYNC and _cuda(output) and _cuda(input) and input.is_contiguous() and output.is_contiguous():
+            return _enqueue(input, output, host, async_op)
+        h = _host(input)
+        output.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
 
     return fn
 
 
 def _wrap_all_gather(orig: Callable[..., Any]) -> Callable[..., Any]:
-    """all_gather(tensor_list, tensor, ...)."""
+    """all_gather(tensor_list, tensor, ...): always through the synchronous path (used outside the step)."""
 
     @functools.wraps(orig)
     def fn(tensor_list: list[torch.Tensor], tensor: torch.Tensor, *args: Any, async_op: bool = False,
            **kwargs: Any) -> Any:
         if not (_cuda(tensor) or any(_cuda(t) for t in tensor_list)):
-            return orig(tensor_list, tensor, *args, async_op=async_op, **kwargs)
+            return _host_call(lambda: orig(tensor_list, tensor, *args, async_op=async_op, **kwargs))
+        h = _host(tensor)
         hl = [torch.empty(t.shape, dtype=t.dtype) for t in tensor_list]
-        orig(hl, _host(tensor), *args, **kwargs)
-        for t, h in zip(tensor_list, hl):
-            t.copy_(h)
+        _host_call(lambda: orig(hl, h, *args, **kwargs))
+        for t, x in zip(tensor_list, hl):
+            t.copy_(x)
         return _Done() if async_op else None
 
     return fn
+
+
+def _wrap_host_only(orig: Callable[..., Any]) -> Callable[..., Any]:
+    """Object collectives / barrier: routed through the worker in asynchronous mode (global gloo order)."""
+
+    @functools.wraps(orig)
+    def fn(*args: Any, **kwargs: Any) -> Any:
+        return _host_call(lambda: orig(*args, **kwargs))
+
+    return fn
+
+
+def _refuse_p2p(*_a: Any, **_k: Any) -> Any:
+    raise RuntimeError("SCALING_AMD_REHEARSAL_ASYNC=1 does not support pipeline p2p (its host staging is synchronous); "
+                       "run pipeline layouts in the synchronous rehearsal")
 
 
 def install() -> None:
@@ -160,7 +371,24 @@ def install() -> None:
     dist.reduce_scatter_tensor = _wrap_reduce_scatter(dist.reduce_scatter_tensor)
     dist.all_gather_into_tensor = _wrap_all_gather_into(dist.all_gather_into_tensor)
     dist.all_gather = _wrap_all_gather(dist.all_gather)
+    if _ASYNC:
+        for name in ("barrier", "gather_object", "broadcast_object_list", "all_gather_object"):
+            _orig[name] = getattr(dist, name)
+            setattr(dist, name, _wrap_host_only(getattr(dist, name)))
+        _orig["destroy_process_group"] = dist.destroy_process_group
+
+        def destroy(*a: Any, **k: Any) -> Any:
+            if "worker" in _state:
+                _state["worker"].drain()
+            return _orig["destroy_process_group"](*a, **k)
+
+        dist.destroy_process_group = destroy
+        dist.batch_isend_irecv = _refuse_p2p
 
 
 def installed() -> bool:
     return _installed
+
+
+def async_mode() -> bool:
+    return _ASYNC

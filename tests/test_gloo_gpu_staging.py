@@ -58,3 +58,44 @@ def test_host_staged_collectives_match_gloo(world):
         assert torch.equal(ag, torch.cat(xs))
         assert torch.equal(bc, xs[1])
         assert torch.equal(lst, torch.stack(xs))
+
+
+def _async_worker(rank: int, world: int, port: int, q) -> None:
+    """Asynchronous rehearsal mode, host side: every gloo call (CPU tensors, objects, barrier) runs on the one worker
+    thread in program order and returns what plain gloo returns."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from scaling_amd.core.topology import gloo_gpu
+
+    gloo_gpu._ASYNC = True
+    gloo_gpu.install()
+    x = torch.arange(8, dtype=torch.float32) + 10 * rank
+    outs = []
+    for i in range(20):  # many small calls back to back: any cross-thread reordering would mismatch the ranks
+        a = x.clone() * (i + 1)
+        dist.all_reduce(a)
+        outs.append(a.tolist())
+    objs = [None] * world
+    dist.all_gather_object(objs, {"rank": rank})
+    dist.barrier()
+    q.put((rank, outs, [o["rank"] for o in objs], gloo_gpu._state["worker"].t.name))
+    dist.destroy_process_group()
+
+
+def test_async_mode_host_calls_through_one_worker():
+    world = 2
+    port = find_free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_async_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    tot = sum((torch.arange(8, dtype=torch.float32) + 10 * r for r in range(world)))
+    for r in range(world):
+        outs, ranks, tname = res[r]
+        assert all(torch.equal(torch.tensor(o), tot * (i + 1)) for i, o in enumerate(outs))
+        assert ranks == list(range(world)) and tname == "gloo-gpu-async"

@@ -271,12 +271,15 @@ def test_gpu_dgrad_transpose_cache_matches_uncached(extra):
 def test_gpu_shard_proxy_emulated_comm():
     """BASELINE #3's per-rank proxy with emulated collectives (each one streams its per-rank send volume through HBM on
     16 CUs and holds them for its modelled xGMI time, asynchronous ones on a proxy stream) trains to the stub run's
-    loss (the emulation moves no data the model reads) and takes longer than the stub run."""
+    loss (the emulation moves no data the model reads) and takes longer than the stub run.  The link efficiency is set
+    so low (SCALING_AMD_PROXY_COMM_EFF) that every TP collective of this small model holds its CUs for ~10-20 ms: the
+    step must grow by at least the blocking ones' sum, which small-model timing noise cannot hide."""
     stub = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8"])
-    emu = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8", "--proxy-comm", "emulate"])
+    emu = _bench_loss({"SCALING_AMD_PROXY_COMM_EFF": "0.00065"},
+                      ["--shard-proxy", "baseline3", "--micro-batch", "8", "--proxy-comm", "emulate"])
     assert emu["proxy_comm"] == "emulate" and stub["proxy_comm"] == "stub"
     assert emu["loss"] == stub["loss"]
-    assert emu["per_rank_ms_per_step"][0] > stub["per_rank_ms_per_step"][0]
+    assert emu["per_rank_ms_per_step"][0] > stub["per_rank_ms_per_step"][0] + 100.0, (emu, stub)
 
 
 def test_gpu_shard_proxy_tp_chunks_match():

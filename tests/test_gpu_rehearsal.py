@@ -114,6 +114,10 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         (["--gpus", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),              # ... running 1 ms late per collective
         (["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_COMM_DELAY_US": "1000"}),
         (["--gpus", "8", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {}),
+        # RCCL lifetimes (core/topology/gloo_gpu.py, asynchronous mode): every collective only enqueued, its input
+        # read and its output written when the stream gets there / the peers are done
+        (["--gpus", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
+        (["--gpus", "4", "--tp", "2", "--sequence-parallel"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):
@@ -133,10 +137,9 @@ def test_race_check_multi_stream_equals_single_stream(args, env):
     the split (profiles/race_forensics_r5.md)."""
     base = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
             "--warmup", "1"]
-    split = {"SCALING_AMD_REHEARSAL_CU_SPLIT": "1"} if args[1] != "1" else {}
     out = {}
     for mode, extra in (("multi", {}), ("single", {"SCALING_AMD_SINGLE_STREAM": "1"})):
-        r = _run([*base, *args], env_extra={**env, **extra, **split, "SCALING_AMD_DETERMINISTIC": "1"}, timeout=300)
+        r = _run([*base, *args], env_extra={**env, **extra, "SCALING_AMD_DETERMINISTIC": "1"}, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
         res = _json_lines(r.stdout)[0]["config"]
         out[mode] = (res["param_checksum"], res["loss"])

@@ -8,10 +8,14 @@ through); wraps ``ops.attention._RopeFlashAttn.bwd_into``:
 * ``ATTN_FORENSICS_TWICE=1``  the same backward two more times into fresh buffers, with the differences recorded
   through ``core/utils/grad_probe.record_values("rope_flash.twice_mismatch", ...)``:
   [total, dq, dk, dv, first 4 flat indices, row length, third == first, third == second, distinct rows, max |diff|,
-  up to 16 distinct columns (-1 padded), first 4 differing values of the first run, then of the second].
+  up to 16 distinct columns (-1 padded), first 4 differing values of the first run, then of the second];
+  with ``ATTN_FORENSICS_OUT=<prefix>`` each rank also writes ``<prefix>.rank<r>.json`` at exit: backwards checked,
+  backwards with any difference, differing elements, largest difference (the rate a candidate fix must bring to 0).
 """
 from __future__ import annotations
 
+import atexit
+import json
 import os
 
 import torch
@@ -22,6 +26,24 @@ from scaling_amd.ops import attention
 _SYNC = os.environ.get("ATTN_FORENSICS_SYNC") == "1"
 _TWICE = os.environ.get("ATTN_FORENSICS_TWICE") == "1"
 _orig = attention._RopeFlashAttn.bwd_into
+_OUT = os.environ.get("ATTN_FORENSICS_OUT")
+_stats: list = []  # per checked backward: the mismatch record (device tensors; read once, at exit)
+
+
+def _summary() -> None:
+    if not _OUT or not _stats:
+        return
+    rows = torch.stack([r[:1] for r in _stats]).reshape(-1).cpu()
+    mx = torch.stack([r[12:13] for r in _stats]).reshape(-1).cpu()
+    third_first = torch.stack([r[9:10] for r in _stats]).reshape(-1).cpu()
+    rank = os.environ.get("RANK", "0")
+    with open(f"{_OUT}.rank{rank}.json", "w") as f:
+        json.dump({"backwards": len(_stats), "with_difference": int((rows > 0).sum()), "elements": float(rows.sum()),
+                   "max_abs_diff": float(mx.max()),
+                   "differing_with_third_equal_first": int(((rows > 0) & (third_first > 0)).sum())}, f)
+
+
+atexit.register(_summary)
 
 
 def _mismatch(dbase: torch.Tensor, d2: torch.Tensor, d3: torch.Tensor, views1, views2) -> torch.Tensor:
@@ -63,7 +85,10 @@ def bwd_into(ctx, do, dq, dk, dv) -> None:
         _orig(ctx, do, *views)
         outs.append((d, views))
     (d2, v2), (d3, _) = outs
-    grad_probe.record_values("rope_flash.twice_mismatch", _mismatch(dbase, d2, d3, (dq, dk, dv), v2))
+    rec = _mismatch(dbase, d2, d3, (dq, dk, dv), v2)
+    grad_probe.record_values("rope_flash.twice_mismatch", rec)
+    if _OUT:
+        _stats.append(rec)
 
 
 attention._RopeFlashAttn.bwd_into = staticmethod(bwd_into)
