@@ -20,3 +20,24 @@ def test_attention_barriers_retire_lds_dma():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "dma_barrier_check.py")], capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_war_rule_walker_on_synthetic_streams():
+    """The WAR walker of tools/dma_barrier_check.py flags an LDS-DMA that can follow a ds_read without an
+    lgkmcnt(0) + s_barrier in between -- on the straight path and through a loop's back-edge -- and passes the safe
+    forms (so the real kernels' 'ok' is not vacuous)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from dma_barrier_check import war_violations
+
+    dma = "buffer_load_dwordx4 v1, s[4:7], 0 offen lds"
+    safe = ["ds_read_b128 v[0:3], v9", "s_waitcnt lgkmcnt(0)", "s_barrier", dma]
+    assert war_violations("f", "k", safe) == []
+    assert war_violations("f", "k", ["ds_read_b128 v[0:3], v9", "s_barrier", dma])  # read not retired before barrier
+    assert war_violations("f", "k", ["ds_read_b128 v[0:3], v9", "s_waitcnt lgkmcnt(0)", dma])  # no barrier
+    assert war_violations("f", "k", [dma]) == []  # prologue
+    # loop: the DMA at the loop head follows the previous iteration's reads through the back-edge
+    loop_bad = [".LBB0_1:", dma, "ds_read_b128 v[0:3], v9", "s_waitcnt lgkmcnt(0)", "s_cbranch_scc1 .LBB0_1"]
+    assert war_violations("f", "k", loop_bad)
+    loop_ok = [".LBB0_1:", dma, "ds_read_b128 v[0:3], v9", "s_waitcnt lgkmcnt(0)", "s_barrier",
+               "s_cbranch_scc1 .LBB0_1"]
+    assert war_violations("f", "k", loop_ok) == []

@@ -1,8 +1,14 @@
-"""Static check of the LDS-DMA hand-off rule in the attention kernels (the race the round-5 gradient trace found).
+"""Static check of the LDS-DMA hand-off rules in the attention kernels (the race the round-5 gradient trace found).
 
-Every ``s_barrier`` after which waves read tiles that OTHER waves staged by LDS-DMA must be preceded, in each wave, by
-an ``s_waitcnt vmcnt(0)`` with no LDS-DMA issue in between (``flash_attn.h: dma_barrier``).  Compiles the kernel files
-to gfx950 assembly (the extension build's flags) and walks back from every barrier of the listed kernels.
+* RAW: every ``s_barrier`` after which waves read tiles that OTHER waves staged by LDS-DMA must be preceded, in each
+  wave, by an ``s_waitcnt vmcnt(0)`` with no LDS-DMA issue in between (``flash_attn.h: dma_barrier``).
+* WAR: no LDS-DMA may be issued into LDS that a wave may still be reading: walking back from every LDS-DMA issue along
+  every control-flow path (fall-through and branches into each block), an ``s_barrier`` must come before any
+  ``ds_read*``, and behind that barrier an ``s_waitcnt ... lgkmcnt(0)`` before any earlier ``ds_read*`` -- so every
+  wave's reads have returned before any wave overwrites (all waves run the same code).  Paths that reach the kernel
+  entry (the prologue) are fine.  Slot-blind, so it is conservative: a DMA into a slot nobody reads would also have to
+  be separated.
+Compiles the kernel files to gfx950 assembly (the extension build's flags) and walks the listed kernels.
 
     python tools/dma_barrier_check.py      # exit 1 and a list of offending barriers on failure
 """
@@ -34,6 +40,7 @@ def check_file(name: str, kernels: tuple[str, ...]) -> list[str]:
         if not any(k in fn for k in kernels):
             continue
         body = s[m.end(): s.index(".Lfunc_end", m.end())].splitlines()
+        bad += war_violations(name, fn, body)
         for n, line in enumerate(body):
             if line.strip() != "s_barrier":
                 continue
@@ -47,13 +54,61 @@ def check_file(name: str, kernels: tuple[str, ...]) -> list[str]:
     return bad
 
 
+_BRANCH = re.compile(r"^s_(?:cbranch_\w+|branch)\s+(\.\w+)")
+
+
+def _is_dma(t: str) -> bool:
+    return t.startswith(("buffer_load", "global_load_lds")) and " lds" in t
+
+
+def war_violations(name: str, fn: str, body: list[str]) -> list[str]:
+    """WAR rule (module docstring) for one kernel body."""
+    lines = [ln.strip() for ln in body]
+    labels = {t[:-1]: i for i, t in enumerate(lines) if re.match(r"^\.\w+:$", t)}
+    sites: dict[str, list[int]] = {}
+    for i, t in enumerate(lines):
+        m = _BRANCH.match(t)
+        if m:
+            sites.setdefault(m.group(1), []).append(i)
+
+    def walk(k: int, barrier: bool, seen: set) -> bool:
+        """True if every path backwards from line k (exclusive) satisfies the rule in state ``barrier``."""
+        while k > 0:
+            k -= 1
+            t = lines[k]
+            if t.endswith(":") and t[:-1] in labels:
+                key = (t[:-1], barrier)
+                if key in seen:
+                    return True
+                seen.add(key)
+                if not all(walk(j, barrier, seen) for j in sites.get(t[:-1], [])):
+                    return False
+                prev = lines[k - 1] if k > 0 else ""
+                if prev.startswith(("s_branch", "s_endpgm")):
+                    return True  # no fall-through into this block
+                continue
+            if t.startswith("ds_read"):
+                return False
+            if not barrier and t == "s_barrier":
+                barrier = True
+            elif barrier and t.startswith("s_waitcnt") and "lgkmcnt(0)" in t:
+                return True
+        return True
+
+    bad = []
+    for i, t in enumerate(lines):
+        if _is_dma(t) and not walk(i, False, set()):
+            bad.append(f"{name}:{fn}: LDS-DMA at line {i} may overwrite LDS that a wave has not finished reading")
+    return bad
+
+
 def main() -> int:
     bad = []
     for f, ks in FILES.items():
         bad += check_file(f, ks)
     for b in bad:
         print(b)
-    print("ok" if not bad else f"{len(bad)} barrier(s) without a DMA-retiring wait")
+    print("ok" if not bad else f"{len(bad)} LDS-DMA hand-off violation(s)")
     return 1 if bad else 0
 
 
