@@ -155,8 +155,13 @@ __device__ __forceinline__ void dma_load(const DmaTile<D, W, R>& t, const void* 
 // wave could read a slower peer's piece of the next tile before it landed (the stale bytes of two tiles ago).  That
 // happened rarely, under load (cdna_hip_programming.md §5 "Read a staged buffer one phase AFTER the wait that retires
 // it"; found by the race check's gradient trace, tools/race_trace.py).
+// race forensics (A/B builds only): SA_DMA_SETTLE = an s_sleep between the DMA-retiring wait and the barrier
+#ifndef SA_DMA_SETTLE
+#define SA_DMA_SETTLE 0
+#endif
 __device__ __forceinline__ void dma_barrier() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (SA_DMA_SETTLE) asm volatile("s_sleep 4" ::: "memory");
     if constexpr ((SA_PROBE & 2) == 0) __syncthreads();  // (timing probe 2: no workgroup barrier -- wrong results)
 }
 

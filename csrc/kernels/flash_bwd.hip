@@ -558,18 +558,23 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
+// race forensics (A/B builds only): extra dynamic LDS per workgroup, so that no second attention workgroup (of this
+// process or another) fits on the CU
+#ifndef SA_FA_BWD_LDS_PAD
+#define SA_FA_BWD_LDS_PAD 0
+#endif
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
-        const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
+        const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512) + SA_FA_BWD_LDS_PAD;
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     {
         dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + 127) / 128);
-        const size_t lds = 4 * 64 * D * 2;
+        const size_t lds = 4 * 64 * D * 2 + SA_FA_BWD_LDS_PAD;
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);

@@ -44,6 +44,15 @@ import torch.distributed as dist
 _installed = False
 _orig: dict[str, Callable[..., Any]] = {}
 _ASYNC = os.environ.get("SCALING_AMD_REHEARSAL_ASYNC", "0") == "1"
+_TRACE = os.environ.get("SCALING_AMD_REHEARSAL_TRACE", "0") == "1"  # debug: every enqueue / gate step to stderr
+
+
+def _trace(msg: str) -> None:
+    if _TRACE:
+        import sys
+
+        print(f"[gloo_gpu r{os.environ.get('RANK', '?')} {threading.current_thread().name}] {msg}", file=sys.stderr,
+              flush=True)
 
 
 class _Done:
@@ -233,15 +242,22 @@ def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[tor
         e_out.record(st)
     _state.setdefault("pinned", []).append((e_out, (h_in, h_out)))
 
+    n = gates.i
+
     def job() -> None:
         try:
+            _trace(f"#{n} start (gate {idx} gen {gen})")
             e_in.synchronize()
+            _trace(f"#{n} input copied out")
             res = host_fn(h_in)
             if res is not h_out:
                 h_out.copy_(res.reshape(h_out.shape))
+            _trace(f"#{n} gloo done")
         finally:  # always open the gate: a failed collective must not leave the stream waiting (the error is raised)
             ext().gate_flag_write(gates.base, idx, gen)
+            _trace(f"#{n} gate open (flag reads {ext().gate_flag_read(gates.base, idx)})")
 
+    _trace(f"#{n} enqueued {tuple(gpu_in.shape)} {gpu_in.dtype} async_op={async_op} on stream {st.stream_id}")
     _worker().submit(job)
     if async_op:
         gpu_in.record_stream(st)
@@ -252,7 +268,12 @@ def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[tor
 
 def _host_call(fn: Callable[[], Any]) -> Any:
     """A gloo call on host tensors / objects: through the worker in asynchronous mode (global order), else direct."""
-    return _worker().call(fn) if _ASYNC and _installed else fn()
+    if not (_ASYNC and _installed):
+        return fn()
+    _trace("host call")
+    out = _worker().call(fn)
+    _trace("host call done")
+    return out
 
 
 # ------------------------------------------------------------------------------------------ wrappers

@@ -1003,3 +1003,21 @@ def test_swiglu_mlp_matches_fp32_reference(T, H, F):
     yf.backward(dy.float().reshape(-1, H))
     for a, r in zip(got, [yf, xf.grad, wg.grad, wu.grad, wd.grad]):
         assert (a.reshape(r.shape) - r).abs().max().item() < 0.03 * r.abs().max().item()
+
+
+def test_xgmi_emulate_moves_bytes_and_holds_time():
+    """The per-rank proxy's emulated collective (ext().xgmi_emulate): the send volume is streamed from the source into
+    the scratch ring (wrapping both), and the kernel holds its CUs until the modelled time has passed."""
+    import time
+
+    src = torch.randn(1 << 16, device=DEV)  # 256 KiB
+    scratch = torch.zeros(1 << 15, device=DEV)  # 128 KiB ring
+    ext().xgmi_emulate(src, scratch, src.numel() * 4, 0.0, 4)  # bytes only
+    torch.cuda.synchronize()
+    # the second half of the source wrapped onto the first: the ring holds src[32768:]
+    assert torch.equal(scratch, src[1 << 15:])
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ext().xgmi_emulate(src, scratch, 1024, 2000.0, 4)  # 2 ms each
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 >= 0.0095

@@ -33,14 +33,18 @@ _stats: list = []  # per checked backward: the mismatch record (device tensors; 
 def _summary() -> None:
     if not _OUT or not _stats:
         return
-    rows = torch.stack([r[:1] for r in _stats]).reshape(-1).cpu()
-    mx = torch.stack([r[12:13] for r in _stats]).reshape(-1).cpu()
-    third_first = torch.stack([r[9:10] for r in _stats]).reshape(-1).cpu()
+    allr = torch.stack([r[:13] for r in _stats]).cpu()  # total, dq, dk, dv, 4 indices, row length, d3==d1, d3==d2, rows, max
+    rows, mx, third_first, third_second = allr[:, 0], allr[:, 12], allr[:, 9], allr[:, 10]
+    diff = rows > 0
     rank = os.environ.get("RANK", "0")
     with open(f"{_OUT}.rank{rank}.json", "w") as f:
         json.dump({"backwards": len(_stats), "with_difference": int((rows > 0).sum()), "elements": float(rows.sum()),
                    "max_abs_diff": float(mx.max()),
-                   "differing_with_third_equal_first": int(((rows > 0) & (third_first > 0)).sum())}, f)
+                   "differing_with_third_equal_first": int((diff & (third_first > 0)).sum()),
+                   "differing_with_third_equal_second": int((diff & (third_second > 0)).sum()),
+                   "elements_dq_dk_dv": [float(allr[:, i].sum()) for i in (1, 2, 3)],
+                   "differing_backward_index": [int(i) for i in torch.nonzero(diff).reshape(-1).tolist()],
+                   "distinct_rows": [int(v) for v in allr[diff, 11].tolist()]}, f)
 
 
 atexit.register(_summary)
