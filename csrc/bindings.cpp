@@ -11,6 +11,8 @@
 #include <vector>
 #include "kernels/launch.h"
 
+void register_rehearsal(pybind11::module& m);  // rehearsal.cpp: asynchronous rehearsal worker
+
 namespace {
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
@@ -738,6 +740,7 @@ at::Tensor dropout_add(const at::Tensor& x_, const c10::optional<at::Tensor>& re
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "scaling_amd CDNA4 (gfx950) HIP kernels";
+    register_rehearsal(m);
     m.def("norm_fwd", &norm_fwd, "RMSNorm/LayerNorm forward (optional fused residual add)", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("layer"), py::arg("res") = py::none());
     m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");

@@ -26,6 +26,33 @@ __device__ __forceinline__ void epi_pad() {
     }
 }
 
+// delta[q] = rowsum(dO * O) with one thread per (token, head) row: no cross-lane reduction (A/B build switch
+// SA_FA_DOT_ROW; race forensics, profiles/race_forensics_r6.md)
+#ifndef SA_FA_DOT_ROW
+#define SA_FA_DOT_ROW 0
+#endif
+template <int D, typename E>
+__global__ __launch_bounds__(256) void fa_bwd_dot_row_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
+                                                             const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
+                                                             float* __restrict__ delta, const float* __restrict__ lse,
+                                                             float* __restrict__ lse2, int64_t T, int H) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= T * H) return;
+    const int64_t t = row / H;
+    const int hh = (int)(row % H);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+        float a[8], b[8];
+        V8<E>::ld(o + t * o_tok + hh * o_head + 8 * c, a);
+        V8<E>::ld(dO + t * d_tok + hh * d_head + 8 * c, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += a[j] * b[j];
+    }
+    delta[(int64_t)hh * T + t] = s;
+    lse2[(int64_t)hh * T + t] = lse[(int64_t)hh * T + t] * 1.4426950408889634f;
+}
+
 template <int D, typename E>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
                                                          const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
@@ -590,6 +617,12 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
 
 template <int D, typename T>
 static void launch_bwd_dot(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, hipStream_t st) {
+    if constexpr (SA_FA_DOT_ROW) {
+        const int grid = (int)((Tq * a.Hq + 255) / 256);
+        hipLaunchKernelGGL((fa_bwd_dot_row_kernel<D, T>), grid, 256, 0, st, (const T*)o, o_tok, o_head, (const T*)a.dO,
+                           a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
+        return;
+    }
     const int64_t threads = Tq * a.Hq * (D / 8);
     const int grid = (int)((threads + 255) / 256);
     hipLaunchKernelGGL((fa_bwd_dot_kernel<D, T>), grid, 256, 0, st, (const T*)o, o_tok, o_head, (const T*)a.dO, a.do_tok,

@@ -58,7 +58,7 @@ def _common_flags(inc: list[str]) -> list[str]:
 
 def _sources() -> list[Path]:
     """Sources of the torch/HIP extension ``_C`` (kernels + bindings)."""
-    return sorted(list((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp"])
+    return sorted(list((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp", CSRC / "rehearsal.cpp"])
 
 
 def _data_sources() -> list[Path]:

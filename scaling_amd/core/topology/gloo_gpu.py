@@ -34,7 +34,6 @@ from __future__ import annotations
 
 import functools
 import os
-import queue
 import threading
 from typing import Any, Callable, Optional
 
@@ -121,54 +120,16 @@ def _h_reduce_scatter(hi: torch.Tensor, out_shape: torch.Size, out_dtype: torch.
 
 
 # ------------------------------------------------------------------------------------------ asynchronous mode
-class _Worker:
-    """Runs every gloo call of this process, in submission (= program) order, on one thread."""
-
-    def __init__(self) -> None:
-        self.q: "queue.Queue[Optional[tuple[Callable[[], Any], Any]]]" = queue.Queue()
-        self.error: Optional[BaseException] = None
-        self.t = threading.Thread(target=self._loop, name="gloo-gpu-async", daemon=True)
-        self.t.start()
-
-    def _loop(self) -> None:
-        while True:
-            item = self.q.get()
-            if item is None:
-                return
-            fn, fut = item
-            try:
-                fut["value"] = fn()
-            except BaseException as e:  # noqa: BLE001 - re-raised on the caller's next call
-                fut["error"] = e
-                self.error = self.error or e
-            finally:
-                fut["done"].set()
-
-    def submit(self, fn: Callable[[], Any]) -> dict[str, Any]:
-        if self.error is not None:
-            raise RuntimeError("asynchronous rehearsal collective failed") from self.error
-        fut: dict[str, Any] = {"done": threading.Event()}
-        self.q.put((fn, fut))
-        return fut
-
-    def call(self, fn: Callable[[], Any]) -> Any:
-        fut = self.submit(fn)
-        fut["done"].wait()
-        if "error" in fut:
-            raise fut["error"]
-        return fut.get("value")
-
-    def drain(self) -> None:
-        self.call(lambda: None)
-
-
+# The worker that runs every gloo call of the rank in program order is C++ (csrc/rehearsal.cpp): a Python thread
+# needs the GIL between its steps, and a main thread blocked in a GIL-holding call on a tensor behind a gate (a
+# .tolist()) deadlocked the rank (profiles/race_forensics_r6.md).
 class _Gates:
     """A ring of flag words; each use of a word waits for the next generation number."""
 
     def __init__(self, n: int = 1 << 14) -> None:
         from ...ops._ext import ext
 
-        kind = int(os.environ.get("SCALING_AMD_REHEARSAL_GATE_KIND", "1"))
+        kind = int(os.environ.get("SCALING_AMD_REHEARSAL_GATE_KIND", "1"))  # 1: coherent pinned host memory
         self.base = ext().gate_flags_alloc(n, kind)
         self.n, self.i = n, 0
         self.gen = [0] * n
@@ -195,12 +156,23 @@ class _AsyncWork:
 
 
 _state: dict[str, Any] = {}
+_KIND = {"all_reduce": 0, "broadcast": 1, "reduce_scatter": 2, "all_gather": 3}
 
 
-def _worker() -> _Worker:
-    if "worker" not in _state:
-        _state["worker"] = _Worker()
-    return _state["worker"]
+def _op_code(op: Any) -> int:
+    if op is None or op == dist.ReduceOp.SUM:
+        return 0
+    if op == dist.ReduceOp.MAX:
+        return 1
+    if op == dist.ReduceOp.MIN:
+        return 2
+    if op == dist.ReduceOp.PRODUCT:
+        return 3
+    raise ValueError(f"asynchronous rehearsal: unsupported reduce op {op}")
+
+
+def _pg(group: Any) -> Any:
+    return group if group is not None else dist.distributed_c10d._get_default_group()
 
 
 def _side_stream(dev: torch.device) -> Any:
@@ -211,16 +183,17 @@ def _side_stream(dev: torch.device) -> Any:
 
 
 def _retire_pinned() -> None:
-    """Drops the pinned staging buffers whose host-to-device copy has completed."""
+    """Drops the staging buffers / events whose host-to-device copy has completed."""
     live = _state.setdefault("pinned", [])
-    live[:] = [(ev, bufs) for ev, bufs in live if not ev.query()]
+    live[:] = [item for item in live if not item[0].query()]
 
 
-def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[torch.Tensor], torch.Tensor],
-             async_op: bool) -> Any:
+def _enqueue(kind: str, gpu_in: torch.Tensor, gpu_out: torch.Tensor, group: Any, op: Any, async_op: bool,
+             root: int = 0) -> Any:
     """RCCL-like collective: input copy-out, gate and result copy-in enqueued on the stream; gloo in the worker."""
     from ...ops._ext import ext
 
+    ext().rw_check()
     if "gates" not in _state:
         _state["gates"] = _Gates()
     gates = _state["gates"]
@@ -229,8 +202,9 @@ def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[tor
     st = _side_stream(gpu_out.device) if async_op else cur
     if async_op:
         st.wait_stream(cur)
+    in_place = gpu_in.data_ptr() == gpu_out.data_ptr() and gpu_in.shape == gpu_out.shape
     h_in = torch.empty(gpu_in.shape, dtype=gpu_in.dtype, pin_memory=True)
-    h_out = torch.empty(gpu_out.shape, dtype=gpu_out.dtype, pin_memory=True)
+    h_out = h_in if in_place else torch.empty(gpu_out.shape, dtype=gpu_out.dtype, pin_memory=True)
     idx, gen = gates.take()
     with torch.cuda.stream(st):
         h_in.copy_(gpu_in, non_blocking=True)  # read when the stream gets here
@@ -240,25 +214,10 @@ def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[tor
         gpu_out.copy_(h_out, non_blocking=True)  # written once the peers are done
         e_out = torch.cuda.Event()
         e_out.record(st)
-    _state.setdefault("pinned", []).append((e_out, (h_in, h_out)))
-
-    n = gates.i
-
-    def job() -> None:
-        try:
-            _trace(f"#{n} start (gate {idx} gen {gen})")
-            e_in.synchronize()
-            _trace(f"#{n} input copied out")
-            res = host_fn(h_in)
-            if res is not h_out:
-                h_out.copy_(res.reshape(h_out.shape))
-            _trace(f"#{n} gloo done")
-        finally:  # always open the gate: a failed collective must not leave the stream waiting (the error is raised)
-            ext().gate_flag_write(gates.base, idx, gen)
-            _trace(f"#{n} gate open (flag reads {ext().gate_flag_read(gates.base, idx)})")
-
-    _trace(f"#{n} enqueued {tuple(gpu_in.shape)} {gpu_in.dtype} async_op={async_op} on stream {st.stream_id}")
-    _worker().submit(job)
+    _state.setdefault("pinned", []).append((e_out, e_in, h_in, h_out))
+    _trace(f"#{gates.i} {kind} {tuple(gpu_in.shape)} {gpu_in.dtype} async_op={async_op} stream {st.stream_id} "
+           f"gate {idx}/{gen}")
+    ext().rw_collective(_KIND[kind], _pg(group), h_in, h_out, _op_code(op), root, e_in.cuda_event, gates.base, idx, gen)
     if async_op:
         gpu_in.record_stream(st)
         gpu_out.record_stream(st)
@@ -267,13 +226,16 @@ def _enqueue(gpu_in: torch.Tensor, gpu_out: torch.Tensor, host_fn: Callable[[tor
 
 
 def _host_call(fn: Callable[[], Any]) -> Any:
-    """A gloo call on host tensors / objects: through the worker in asynchronous mode (global order), else direct."""
+    """A gloo call on host tensors / objects: in asynchronous mode in its program-order turn among the worker's jobs."""
     if not (_ASYNC and _installed):
         return fn()
-    _trace("host call")
-    out = _worker().call(fn)
-    _trace("host call done")
-    return out
+    from ...ops._ext import ext
+
+    ticket = ext().rw_host_begin()
+    try:
+        return fn()
+    finally:
+        ext().rw_host_end(ticket)
 
 
 # ------------------------------------------------------------------------------------------ wrappers
@@ -283,7 +245,7 @@ def _wrap_all_reduce(orig: Callable[..., Any]) -> Callable[..., Any]:
         if not _cuda(tensor):
             return _host_call(lambda: orig(tensor, _op(op), group, async_op))
         if _ASYNC and tensor.is_contiguous():
-            return _enqueue(tensor, tensor, lambda h: _h_all_reduce(h, op, group), async_op)
+            return _enqueue("all_reduce", tensor, tensor, group, op, async_op)
         h = _host(tensor)
         tensor.copy_(_host_call(lambda: _h_all_reduce(h, op, group)))
         return _Done() if async_op else None
@@ -302,7 +264,10 @@ def _wrap_broadcast(orig: Callable[..., Any]) -> Callable[..., Any]:
             return h
 
         if _ASYNC and tensor.is_contiguous():
-            return _enqueue(tensor, tensor, host, async_op)
+            src = args[0] if args else kwargs.get("src", 0)
+            group = args[1] if len(args) > 1 else kwargs.get("group")
+            root = dist.get_group_rank(group, src) if group is not None else src
+            return _enqueue("broadcast", tensor, tensor, group, None, async_op, root=root)
         h = _host(tensor)
         tensor.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
@@ -318,7 +283,7 @@ def _wrap_reduce_scatter(orig: Callable[..., Any]) -> Callable[..., Any]:
             return _host_call(lambda: orig(output, input, _op(op), group, async_op))
         host = lambda h: _h_reduce_scatter(h, output.shape, output.dtype, op, group)  # noqa: E731
         if _ASYNC and _cuda(output) and _cuda(input) and input.is_contiguous() and output.is_contiguous():
-            return _enqueue(input, output, host, async_op)
+            return _enqueue("reduce_scatter", input, output, group, op, async_op)
         h = _host(input)
         output.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
@@ -338,7 +303,8 @@ def _wrap_all_gather_into(orig: Callable[..., Any]) -> Callable[..., Any]:
             return ho
 
         if _ASYNC and _cuda(output) and _cuda(input) and input.is_contiguous() and output.is_contiguous():
-            return _enqueue(input, output, host, async_op)
+            group = args[0] if args else kwargs.get("group")
+            return _enqueue("all_gather", input, output, group, None, async_op)
         h = _host(input)
         output.copy_(_host_call(lambda: host(h)))
         return _Done() if async_op else None
@@ -399,8 +365,10 @@ def install() -> None:
         _orig["destroy_process_group"] = dist.destroy_process_group
 
         def destroy(*a: Any, **k: Any) -> Any:
-            if "worker" in _state:
-                _state["worker"].drain()
+            from ...ops._ext import ext
+
+            ext().rw_drain()
+            ext().rw_check()
             return _orig["destroy_process_group"](*a, **k)
 
         dist.destroy_process_group = destroy

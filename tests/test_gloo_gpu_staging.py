@@ -61,28 +61,45 @@ def test_host_staged_collectives_match_gloo(world):
 
 
 def _async_worker(rank: int, world: int, port: int, q) -> None:
-    """Asynchronous rehearsal mode, host side: every gloo call (CPU tensors, objects, barrier) runs on the one worker
-    thread in program order and returns what plain gloo returns."""
+    """Asynchronous rehearsal mode, host side: the C++ worker (csrc/rehearsal.cpp) runs queued collectives on the
+    group's ProcessGroup in program order and opens each job's gate word; Python-level gloo calls (CPU tensors, objects,
+    barrier) take their turn between them.  Here the gate words are a CPU tensor and the jobs have no event."""
+    import time
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from scaling_amd.core.topology import gloo_gpu
+    from scaling_amd.ops._ext import ext
 
     gloo_gpu._ASYNC = True
     gloo_gpu.install()
     x = torch.arange(8, dtype=torch.float32) + 10 * rank
-    outs = []
-    for i in range(20):  # many small calls back to back: any cross-thread reordering would mismatch the ranks
+    flags = torch.zeros(64, dtype=torch.int32)
+    pg = dist.distributed_c10d._get_default_group()
+    hs = []
+    for i in range(20):  # C++ jobs interleaved with Python-level calls: any reordering would mismatch the ranks
+        h = x.clone() * (i + 1)
+        ext().rw_collective(0, pg, h, h, 0, 0, 0, flags.data_ptr(), i, 1)  # all_reduce SUM, gate word i
+        hs.append(h)
         a = x.clone() * (i + 1)
-        dist.all_reduce(a)
-        outs.append(a.tolist())
+        dist.all_reduce(a)  # Python-level gloo call in its turn
+    g = torch.empty(8 * world)
+    ext().rw_collective(3, pg, x.clone(), g, 0, 0, 0, flags.data_ptr(), 20, 1)  # all_gather_into
+    m = x.clone()
+    ext().rw_collective(0, pg, m, m, 1, 0, 0, flags.data_ptr(), 21, 1)  # all_reduce MAX
     objs = [None] * world
     dist.all_gather_object(objs, {"rank": rank})
     dist.barrier()
-    q.put((rank, outs, [o["rank"] for o in objs], gloo_gpu._state["worker"].t.name))
+    ext().rw_drain()
+    ext().rw_check()
+    t0 = time.time()
+    while int(flags[:22].min()) < 1 and time.time() - t0 < 30:
+        time.sleep(0.01)
+    q.put((rank, [h.tolist() for h in hs], g.tolist(), m.tolist(), [o["rank"] for o in objs], flags[:22].tolist()))
     dist.destroy_process_group()
 
 
-def test_async_mode_host_calls_through_one_worker():
+def test_async_mode_worker_orders_jobs_and_host_calls():
     world = 2
     port = find_free_port()
     ctx = mp.get_context("spawn")
@@ -94,8 +111,11 @@ def test_async_mode_host_calls_through_one_worker():
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    tot = sum((torch.arange(8, dtype=torch.float32) + 10 * r for r in range(world)))
+    xs = [torch.arange(8, dtype=torch.float32) + 10 * r for r in range(world)]
+    tot = sum(xs[1:], xs[0].clone())
     for r in range(world):
-        outs, ranks, tname = res[r]
-        assert all(torch.equal(torch.tensor(o), tot * (i + 1)) for i, o in enumerate(outs))
-        assert ranks == list(range(world)) and tname == "gloo-gpu-async"
+        hs, g, m, ranks, flags = res[r]
+        assert all(torch.equal(torch.tensor(h), tot * (i + 1)) for i, h in enumerate(hs))
+        assert torch.equal(torch.tensor(g), torch.cat(xs))
+        assert torch.equal(torch.tensor(m), torch.maximum(xs[0], xs[1]))
+        assert ranks == list(range(world)) and flags == [1] * 22

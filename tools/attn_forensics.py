@@ -10,7 +10,10 @@ through); wraps ``ops.attention._RopeFlashAttn.bwd_into``:
   [total, dq, dk, dv, first 4 flat indices, row length, third == first, third == second, distinct rows, max |diff|,
   up to 16 distinct columns (-1 padded), first 4 differing values of the first run, then of the second];
   with ``ATTN_FORENSICS_OUT=<prefix>`` each rank also writes ``<prefix>.rank<r>.json`` at exit: backwards checked,
-  backwards with any difference, differing elements, largest difference (the rate a candidate fix must bring to 0).
+  backwards with any difference, differing elements, largest difference (the rate a candidate fix must bring to 0);
+* ``ATTN_FORENSICS_NOROPE=1`` every checked computation (the production one too) runs WITHOUT the inverse RoPE of
+  dq / dk (plain attention backward; training numbers are then wrong, the comparison is not): tells whether a
+  difference comes from the rotation pass or from the attention kernels.
 """
 from __future__ import annotations
 
@@ -25,7 +28,20 @@ from scaling_amd.ops import attention
 
 _SYNC = os.environ.get("ATTN_FORENSICS_SYNC") == "1"
 _TWICE = os.environ.get("ATTN_FORENSICS_TWICE") == "1"
-_orig = attention._RopeFlashAttn.bwd_into
+_NOROPE = os.environ.get("ATTN_FORENSICS_NOROPE") == "1"
+_orig_rope = attention._RopeFlashAttn.bwd_into
+
+
+def _orig(ctx, do, dq, dk, dv) -> None:
+    if not _NOROPE:
+        return _orig_rope(ctx, do, dq, dk, dv)
+    from scaling_amd.ops._ext import ext
+
+    base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
+    specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
+    v = attention._view(base, specs[2])
+    ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
+                 local_heads)
 _OUT = os.environ.get("ATTN_FORENSICS_OUT")
 _stats: list = []  # per checked backward: the mismatch record (device tensors; read once, at exit)
 
@@ -44,7 +60,8 @@ def _summary() -> None:
                    "differing_with_third_equal_second": int((diff & (third_second > 0)).sum()),
                    "elements_dq_dk_dv": [float(allr[:, i].sum()) for i in (1, 2, 3)],
                    "differing_backward_index": [int(i) for i in torch.nonzero(diff).reshape(-1).tolist()],
-                   "distinct_rows": [int(v) for v in allr[diff, 11].tolist()]}, f)
+                   "distinct_rows": [int(v) for v in allr[diff, 11].tolist()],
+                   "first_differing_token": [int(v) for v in (allr[diff, 4] // allr[diff, 8]).tolist()]}, f)
 
 
 atexit.register(_summary)

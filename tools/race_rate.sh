@@ -13,8 +13,8 @@ for b in tree ${VARIANTS}; do
     [ "$b" != tree ] && so="$R/variants/$b.so"
     echo "[race_rate] $b $(date +%T)"
     SCALING_AMD_EXT_SO=$so SCALING_AMD_DEBUG_HOOKS=tools/attn_forensics.py ATTN_FORENSICS_TWICE=1 \
-        ATTN_FORENSICS_OUT="$D/$b" SCALING_AMD_DETERMINISTIC=1 ${EXTRA_ENV} \
-        timeout -k 10 ${RATE_TIMEOUT:-300} python -u bench.py --model llama_tiny --backend gloo-gpu --gpus 2 --seq-len 256 \
+        ATTN_FORENSICS_OUT="$D/$b" SCALING_AMD_DETERMINISTIC=1 env ${EXTRA_ENV} \
+        timeout -k 10 ${RATE_TIMEOUT:-300} python -u bench.py --model llama_tiny --backend gloo-gpu --gpus ${GPUS:-2} --seq-len 256 \
         --micro-batch 2 --steps ${STEPS:-200} --warmup 2 > "$D/$b.log" 2>&1
     cat "$D/$b".rank*.json; echo
 done
