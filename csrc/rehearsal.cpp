@@ -16,6 +16,8 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <functional>
 #include <mutex>
@@ -23,6 +25,17 @@
 #include <thread>
 
 namespace {
+
+const bool kTrace = [] {
+    const char* e = std::getenv("SCALING_AMD_REHEARSAL_TRACE");
+    return e != nullptr && e[0] == '1';
+}();
+void trace(const char* what, int64_t idx, int64_t kind) {
+    if (!kTrace) return;
+    const char* r = std::getenv("RANK");
+    std::fprintf(stderr, "[rehearsal worker r%s] %s job gate %lld kind %lld\n", r ? r : "?", what, (long long)idx,
+                 (long long)kind);
+}
 
 struct Worker {
     std::mutex m;
@@ -137,11 +150,14 @@ void run(int64_t kind, const c10::intrusive_ptr<c10d::ProcessGroup>& pg, at::Ten
 void rw_collective(int64_t kind, const c10::intrusive_ptr<c10d::ProcessGroup>& pg, at::Tensor h_in, at::Tensor h_out,
                    int64_t op, int64_t root, int64_t event, int64_t base, int64_t idx, int64_t gen) {
     worker().push([=]() {
+        trace("start", idx, kind);
         try {
             if (event != 0)  // 0: host-only job (the CPU tests of the worker)
                 TORCH_CHECK(hipEventSynchronize(reinterpret_cast<hipEvent_t>((uintptr_t)event)) == hipSuccess,
                             "rehearsal worker: hipEventSynchronize");
+            trace("input out", idx, kind);
             run(kind, pg, h_in, h_out, op, root);
+            trace("collective done", idx, kind);
         } catch (const std::exception& e) {
             fail(e.what());
         } catch (...) {

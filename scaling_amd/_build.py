@@ -88,7 +88,15 @@ def _check_kernel_stubs(so: Path) -> None:
 # otherwise packs pairs of the softmax's f32 adds / muls into v_pk_*_f32, which beside MFMAs cost more issue cycles
 # than the two scalar instructions they replace (MI355X_MICROARCH.md, "price of one filler"); forward 879-887 ->
 # 897-903 TF at the 7B shape, interleaved A/B, profiles/attn_slp_ab_r5.log.  The backward kernels measured neutral.
-_FILE_FLAGS: dict[str, list[str]] = {"flash_fwd.hip": ["-fno-slp-vectorize"]}
+#
+# The training-path kernels with fp32 arithmetic are all built without SLP vectorisation, for reproducibility: with the
+# SLP-packed build (v_pk_mul_f32 / v_pk_fma_f32 with op_sel / neg modifiers) the inverse-RoPE pass of the attention
+# backward returned a different last bit in 2-8 % of backwards whenever another process's waves shared the GPU (0 of
+# 408 with the RoPE kernels unpacked, 16 of 408 packed in the same run; profiles/race_forensics_r6.md).  The
+# decode-only GEMV / flash-decoding kernels keep SLP (their packed dot products are their speed).
+_NO_SLP = ["-fno-slp-vectorize"]
+_FILE_FLAGS: dict[str, list[str]] = {f: _NO_SLP for f in ("flash_fwd.hip", "flash_bwd.hip", "swiglu_rope.hip", "norm.hip",
+                                                           "xent_embed_optim.hip", "elementwise.hip")}
 
 
 def _env_file_flags() -> dict[str, list[str]]:

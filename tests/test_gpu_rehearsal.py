@@ -117,7 +117,7 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         # RCCL lifetimes (core/topology/gloo_gpu.py, asynchronous mode): every collective only enqueued, its input
         # read and its output written when the stream gets there / the peers are done
         (["--gpus", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
-        (["--gpus", "4", "--tp", "2", "--sequence-parallel"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
+        (["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1", "SCALING_AMD_COMM_DELAY_US": "1000"}),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):
