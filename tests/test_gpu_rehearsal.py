@@ -125,16 +125,17 @@ def test_race_check_multi_stream_equals_single_stream(args, env):
     optional weight-gradient stream, per-layer event waits) must leave bit-identical parameters and losses to
     the same run with every side stream folded onto the compute stream (SCALING_AMD_SINGLE_STREAM=1).  A missing
     stream / event dependency shows up as a different checksum -- and so does any kernel whose result depends on
-    timing: the delayed and 8-rank cases were xfail in round 4 until the gradient trace (tools/race_trace.py, probes
-    in core/utils/grad_probe.py) pinned their divergence on the attention backward, whose loop barriers did not retire
-    every wave's LDS-DMA pieces of the next tile (flash_attn.h: dma_barrier; tools/dma_barrier_check.py).  Both runs use library-side determinism
-    (SCALING_AMD_DETERMINISTIC=1: torch deterministic algorithms, rocBLAS without atomics): with several ranks sharing
-    the one GPU, the default vendor GEMM kernels' atomic accumulation order varies from run to run even with every
-    stream folded (profiles/race_repeat_dp2_r4.log), which would hide what this test checks.  Several ranks run each on
-    a disjoint CU range (SCALING_AMD_REHEARSAL_CU_SPLIT, bench.py), as each would own a GPU: with two ranks' waves
-    co-resident on one CU, ~0.2-1 % of attention backwards came out <= 1 bf16 ulp different from the same backward
-    recomputed in place (a third computation agreeing with the first; no stream of the process involved), 0 of 768 with
-    the split (profiles/race_forensics_r5.md)."""
+    timing.  Both runs use library-side determinism (SCALING_AMD_DETERMINISTIC=1: torch deterministic algorithms,
+    rocBLAS without atomics): with several ranks sharing the one GPU, the default vendor GEMM kernels' atomic
+    accumulation order varies from run to run (profiles/race_repeat_dp2_r4.log).
+
+    History: round 5 fixed a cross-wave LDS-DMA race in the attention loops (flash_attn.h: dma_barrier) and then ran the
+    multi-rank cases on disjoint CU ranges; round 6 found what the ranks' shared CUs exposed: the SLP-packed fp32
+    rotation of the RoPE kernels (v_pk_mul/fma_f32 with operand-select modifiers) returned a different last bit in
+    2-8 % of attention backwards when another process's waves shared the GPU, 0 % built unpacked
+    (profiles/race_forensics_r6.md) -- so every multi-rank case runs on shared CUs again.  The SCALING_AMD_REHEARSAL_ASYNC
+    cases run the collectives with RCCL's lifetimes (core/topology/gloo_gpu.py): inputs read and outputs written when
+    the stream gets there, long after the call returned, so a missing record_stream / early free shows up too."""
     base = ["--model", "llama_tiny", "--backend", "gloo-gpu", "--seq-len", "256", "--micro-batch", "2", "--steps", "3",
             "--warmup", "1"]
     out = {}
