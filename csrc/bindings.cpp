@@ -612,13 +612,8 @@ std::vector<at::Tensor> fa_bwd(const at::Tensor& dout, const at::Tensor& q, cons
                           q.scalar_type() == at::kHalf, cur_stream());
     if (rope && !fold) {
         const int64_t* pp = rope_pos.has_value() ? rope_pos->data_ptr<int64_t>() : nullptr;
-#ifndef SA_ROPE_BWD_MODE
-#define SA_ROPE_BWD_MODE 0  // race forensics A/B only: 1 = stream sync first, 2 = out of place + copy back
-#endif
-        if (SA_ROPE_BWD_MODE == 1) TORCH_CHECK(hipStreamSynchronize(cur_stream()) == hipSuccess);
         for (at::Tensor* t : {&dq, &dk}) {
-            at::Tensor src = SA_ROPE_BWD_MODE == 2 ? t->clone() : *t;
-            sa_launch::rope(dt(*t), rope_interleaved, src.data_ptr(), src.stride(0), src.stride(1), t->data_ptr(),
+            sa_launch::rope(dt(*t), rope_interleaved, t->data_ptr(), t->stride(0), t->stride(1), t->data_ptr(),
                             t->stride(0), t->stride(1), rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), pp,
                             t->size(0), (int)t->size(1), (int)t->size(2), (int)rope_dim, (int)rope_seq, -1.f,
                             cur_stream());

@@ -113,11 +113,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, ui
 // global chunk that belongs at its linear LDS position (source-permuted swizzle).  Rows past the
 // resource range land as zeros.  No staging registers, no ds_write; completion is the vmcnt(0)
 // the compiler places before the next __syncthreads().
-// timing probes for A/B builds only (results are wrong): bit 0 = LDS-DMA loads out of range (no memory traffic),
-// bit 1 = dma_barrier without the workgroup barrier, bit 2 = every DMA re-reads the loop's first tile (L2 hits)
-#ifndef SA_PROBE
-#define SA_PROBE 0
-#endif
 typedef __attribute__((address_space(3))) void lds_void;
 template <int D, int W, int ROWS = 64>
 struct DmaTile {
@@ -134,7 +129,6 @@ struct DmaTile {
         }
     }
     __device__ __forceinline__ void load(const void* base, int64_t tok, int rows, char* tile, int wave_u) const {
-        if constexpr ((SA_PROBE & 1) != 0) rows = 0;  // timing probe: every load out of range (no memory traffic)
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(base, (uint32_t)max(rows, 0) * (uint32_t)tok * 2u);
 #pragma unroll
         for (int i = 0; i < NPW; ++i)
@@ -155,14 +149,9 @@ __device__ __forceinline__ void dma_load(const DmaTile<D, W, R>& t, const void* 
 // wave could read a slower peer's piece of the next tile before it landed (the stale bytes of two tiles ago).  That
 // happened rarely, under load (cdna_hip_programming.md §5 "Read a staged buffer one phase AFTER the wait that retires
 // it"; found by the race check's gradient trace, tools/race_trace.py).
-// race forensics (A/B builds only): SA_DMA_SETTLE = an s_sleep between the DMA-retiring wait and the barrier
-#ifndef SA_DMA_SETTLE
-#define SA_DMA_SETTLE 0
-#endif
 __device__ __forceinline__ void dma_barrier() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (SA_DMA_SETTLE) asm volatile("s_sleep 4" ::: "memory");
-    if constexpr ((SA_PROBE & 2) == 0) __syncthreads();  // (timing probe 2: no workgroup barrier -- wrong results)
+    __syncthreads();
 }
 
 // 3-way max without the canonicalising v_max the compiler wraps around fmaxf

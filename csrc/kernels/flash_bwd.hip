@@ -14,45 +14,6 @@
 using namespace sa;
 using namespace sa::fa;
 
-// race forensics: pad between the last MFMAs of a kernel and its epilogue's reads of their accumulators
-#ifndef SA_FA_BWD_EPI_PAD
-#define SA_FA_BWD_EPI_PAD 0
-#endif
-__device__ __forceinline__ void epi_pad() {
-    if constexpr (SA_FA_BWD_EPI_PAD) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// delta[q] = rowsum(dO * O) with one thread per (token, head) row: no cross-lane reduction (A/B build switch
-// SA_FA_DOT_ROW; race forensics, profiles/race_forensics_r6.md)
-#ifndef SA_FA_DOT_ROW
-#define SA_FA_DOT_ROW 0
-#endif
-template <int D, typename E>
-__global__ __launch_bounds__(256) void fa_bwd_dot_row_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
-                                                             const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
-                                                             float* __restrict__ delta, const float* __restrict__ lse,
-                                                             float* __restrict__ lse2, int64_t T, int H) {
-    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= T * H) return;
-    const int64_t t = row / H;
-    const int hh = (int)(row % H);
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < D / 8; ++c) {
-        float a[8], b[8];
-        V8<E>::ld(o + t * o_tok + hh * o_head + 8 * c, a);
-        V8<E>::ld(dO + t * d_tok + hh * d_head + 8 * c, b);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += a[j] * b[j];
-    }
-    delta[(int64_t)hh * T + t] = s;
-    lse2[(int64_t)hh * T + t] = lse[(int64_t)hh * T + t] * 1.4426950408889634f;
-}
-
 template <int D, typename E>
 __global__ __launch_bounds__(256) void fa_bwd_dot_kernel(const E* __restrict__ o, int64_t o_tok, int64_t o_head,
                                                          const E* __restrict__ dO, int64_t d_tok, int64_t d_head,
@@ -245,7 +206,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
     // work item (q head h0 + gi, query tile qlo + QT qi), qi fastest; the issue and compute cursors advance
     // incrementally (no runtime divisions in the loop)
     auto issue = [&](int gi, int qi, char* buf) {
-        const int qt = (SA_PROBE & 4) ? qlo : qlo + qi * QT, hq = (SA_PROBE & 4) ? h0 : h0 + gi;  // probe 4: first item
+        const int qt = qlo + qi * QT, hq = h0 + gi;
         dma_load(tq, a.q + (int64_t)(q0s + qt) * a.q_tok + (int64_t)hq * a.q_head, a.q_tok, Lq - qt, buf, wave);
         dma_load(td, a.dO + (int64_t)(q0s + qt) * a.do_tok + (int64_t)hq * a.do_head, a.do_tok, Lq - qt, buf + TILE, wave);
         if (wave == 0) {  // QT lse2 then QT delta (lanes past QT read out of range -> zeros into the pad)
@@ -379,7 +340,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dkdv_kernel(BwdArgs a) {
         dma_barrier();
     }
     if (w < nwork) tile(buf0, cg, cq);
-    epi_pad();
 
     if (mykey < Lk) {
         if (a.hsplit > 1) {  // fp32 partials, summed by fa_bwd_reduce_kernel
@@ -476,7 +436,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     //  hipcc's host pass treat the kernel as undefined and drop its launch stub)
 #define SA_DQ_ISSUE(KT, BUFP)                                                                          \
     do {                                                                                               \
-        const int kp_ = (SA_PROBE & 4) ? klo : (KT); /* timing probe 4: always the first tile */        \
+        const int kp_ = (KT);                                                                          \
         dma_load(tk, kbase + (int64_t)kp_ * a.k_tok, a.k_tok, Lk - kp_, (BUFP), wave_u);                 \
         dma_load(tv, vbase + (int64_t)kp_ * a.v_tok, a.v_tok, Lk - kp_, (BUFP) + TILE, wave_u);          \
     } while (0)
@@ -550,7 +510,6 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs a) {
     }
     if (ntiles & 1) tile(buf0, kt);
 #undef SA_DQ_ISSUE
-    epi_pad();
     if (myq < Lq)
         store_grad_row<D, F16>(a, dq, a.scale, q0s + myq, h,
                                a.dq + (int64_t)(q0s + myq) * a.dq_tok + (int64_t)hq * a.dq_head);
@@ -585,23 +544,18 @@ __global__ __launch_bounds__(256) void fa_bwd_reduce_kernel(BwdArgs a) {
     *reinterpret_cast<u16x8*>(a.dv + tok * a.dv_tok + (int64_t)hk * a.dv_head + 8 * c) = wv;
 }
 
-// race forensics (A/B builds only): extra dynamic LDS per workgroup, so that no second attention workgroup (of this
-// process or another) fits on the CU
-#ifndef SA_FA_BWD_LDS_PAD
-#define SA_FA_BWD_LDS_PAD 0
-#endif
 template <bool F16, bool DROP>
 static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipStream_t st) {
     {
         dim3 grid(a.Hkv * a.hsplit, a.nseg, (max_k + 127) / 128);
-        const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512) + SA_FA_BWD_LDS_PAD;
+        const size_t lds = 128 * D * 2 + 2 * (2 * 32 * D * 2 + 512);
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dkdv_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dkdv_kernel<32, F16, DROP>), grid, 256, lds, st, a);
     }
     {
         dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + 127) / 128);
-        const size_t lds = 4 * 64 * D * 2 + SA_FA_BWD_LDS_PAD;
+        const size_t lds = 4 * 64 * D * 2;
         if (D == 128) hipLaunchKernelGGL((fa_bwd_dq_kernel<128, F16, DROP>), grid, 256, lds, st, a);
         else if (D == 64) hipLaunchKernelGGL((fa_bwd_dq_kernel<64, F16, DROP>), grid, 256, lds, st, a);
         else hipLaunchKernelGGL((fa_bwd_dq_kernel<32, F16, DROP>), grid, 256, lds, st, a);
@@ -617,12 +571,6 @@ static void launch_bwd_main(const BwdArgs& a, int D, int max_q, int max_k, hipSt
 
 template <int D, typename T>
 static void launch_bwd_dot(const BwdArgs& a, const uint16_t* o, int64_t o_tok, int64_t o_head, int64_t Tq, hipStream_t st) {
-    if constexpr (SA_FA_DOT_ROW) {
-        const int grid = (int)((Tq * a.Hq + 255) / 256);
-        hipLaunchKernelGGL((fa_bwd_dot_row_kernel<D, T>), grid, 256, 0, st, (const T*)o, o_tok, o_head, (const T*)a.dO,
-                           a.do_tok, a.do_head, a.delta, a.lse, a.lse2, Tq, a.Hq);
-        return;
-    }
     const int64_t threads = Tq * a.Hq * (D / 8);
     const int grid = (int)((threads + 255) / 256);
     hipLaunchKernelGGL((fa_bwd_dot_kernel<D, T>), grid, 256, 0, st, (const T*)o, o_tok, o_head, (const T*)a.dO, a.do_tok,
