@@ -16,7 +16,7 @@ def _case():
 
     from scaling_amd.core.nn.linear import ColumnParallelLinear, main_grad
     from scaling_amd.core.nn.linear.fused import fused_column_linear
-    from scaling_amd.parallel.tp import copy_to_tensor_model_parallel_region
+    from scaling_amd.core.nn.linear.utils import copy_to_tensor_model_parallel_region
 
     topo = make_topology(model_parallel_size=2)
     torch.manual_seed(0)  # same input on both ranks, as in a TP group
