@@ -183,28 +183,25 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs a) {
 //    representable in bf16);
 //  * lane^32 exchanges through v_permlane32_swap;
 //  * masking only on boundary tiles, as 1-2 compares against per-lane bounds.
-template <int D, int NW_ = 4, int KT_ = 64>
+template <int D, int NW_ = 4>
 struct FwdV2 {
-    static constexpr int NW = NW_, BM = 32 * NW, KT = KT_, NB = KT / 32, TILE = KT * D * 2, NKS = D / 16, NT = D / 32;
+    static constexpr int NW = NW_, BM = 32 * NW, KT = 64, TILE = KT * D * 2, NKS = D / 16, NT = D / 32;
     static constexpr float TH = 8.f;
 };
 
 // Variants measured against this one and dropped (8 waves per workgroup, inline-asm LDS-DMA, pinned read-ahead, an
 // 8-wave ping-pong schedule): profiles/attn_fwd_waves_ab_r2.log, attn_fwd_pingpong_ab_r3.log, attn_ab_r2_asyncdma.log;
-// their code is in git history before commit "Delete losing attention variants".
+// their code is in git history before commit "Delete losing attention variants".  128-key tiles (8 waves x 32 queries,
+// 128 KiB of LDS, one workgroup per CU, causal tiles past a wave's queries skipped): 1.28 vs 1.13 ms at the 7B shape,
+// profiles/attn_fwd_kt128_ab_r6.log (code in git history, commit "Drop the race-forensics build switches").
 // NW = 4: 2 workgroups / CU = 2 waves / SIMD; NW = 6 (BM = 192): 2 workgroups / CU = 3 waves / SIMD (<= 168 VGPRs)
-// KT = 128 (SA_FWD_KT, with NW = 8: 128 KiB of LDS, one 8-wave workgroup per CU = 2 waves / SIMD): half the per-tile
-// fixed cost (exchanges, barriers, DMA issue) per key, K / V tiles shared by 256 queries
 #ifndef SA_FWD_NW
 #define SA_FWD_NW 4
 #endif
-#ifndef SA_FWD_KT
-#define SA_FWD_KT 64
-#endif
-template <int D, bool F16, bool DROP, int NW, int KT>
-__global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(FwdArgs a) {
+template <int D, bool F16, bool DROP, int NW>
+__global__ __launch_bounds__(64 * NW, NW / 2) void fa_fwd_v2_kernel(FwdArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass only needs the signature for the launch stub
-    using C = FwdV2<D, NW, KT>;
+    using C = FwdV2<D, NW>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // grid (Hq, nseg, q tiles): the dispatcher walks x fastest, so the tile index is the slowest
     // dimension and causal work is issued heaviest-first across all heads (LPT balance)
@@ -237,7 +234,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
     lo.init(lane);
     // K / V tiles by LDS-DMA (no staging registers); rows past the segment land as zeros
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    DmaTile<D, C::NW, C::KT> tk, tv;
+    DmaTile<D, C::NW> tk, tv;
     tk.init(wave_u, lane, a.k_tok);
     tv.init(wave_u, lane, a.v_tok);
     const u16* kbase = a.k + (int64_t)k0s * a.k_tok + (int64_t)hk * a.k_head;
@@ -269,23 +266,19 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
     if constexpr (DROP) drow = drop_row(drop_head(a.seed, hq), q0s + myq);
 
     auto tile = [&](const char* K, int kt) {
-        if constexpr (C::KT > 64)  // causal: a tile past every query of this wave adds exactly nothing (wave-uniform)
-            if (a.causal && kt > qw0 + 31 + off) return;
         const char* V = K + C::TILE;
-        f32x16 s[C::NB];
-#pragma unroll
-        for (int b = 0; b < C::NB; ++b) s[b] = f32x16{};
+        f32x16 s[2] = {f32x16{}, f32x16{}};
         {
 #pragma unroll
             for (int ks = 0; ks < C::NKS; ++ks)
 #pragma unroll
-                for (int b = 0; b < C::NB; ++b)
+                for (int b = 0; b < 2; ++b)
                     s[b] = mma<F16>(*reinterpret_cast<const bf16x8*>(K + 32 * b * D * 2 + lo.row(ks)), qf[ks], s[b]);
             // one K fragment read per MFMA.  Reading them 4 MFMAs ahead (or interleaving the softmax of the previous
             // tile into these MFMAs) was measured slower: at two waves per SIMD the loop is bound by the SIMD's issue
             // slots, not by LDS latency (profiles/attn_sched_ab_r4.log)
 #pragma unroll
-            for (int i = 0; i < C::NB * C::NKS; ++i) {
+            for (int i = 0; i < 2 * C::NKS; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
             }
@@ -297,7 +290,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
         if (need_mask) {
             mask_fence();
 #pragma unroll
-            for (int b = 0; b < C::NB; ++b) {
+            for (int b = 0; b < 2; ++b) {
                 const int base = kt + 32 * b + 4 * h;  // key of register j = base + crow(j)
                 int hi = Lk - 1 - base;
                 if (a.causal) hi = min(hi, myq + off - base);
@@ -308,14 +301,8 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
             }
         }
         // two independent 16-element chains, one statement each (no hazard pads inside)
-        float mx;
-        if constexpr (C::NB == 2) {
-            const float m0 = vmax16(s[0]), m1 = vmax16(s[1]);
-            mx = vmax3(m0, m1, m1);
-        } else {
-            const float m0 = vmax16(s[0]), m1 = vmax16(s[1]), m2 = vmax16(s[2]), m3 = vmax16(s[3]);
-            mx = vmax3(vmax3(m0, m1, m2), m3, m3);
-        }
+        const float m0 = vmax16(s[0]), m1 = vmax16(s[1]);
+        const float mx = vmax3(m0, m1, m1);
         const float mrow = max_xchg32(mx) * c2;
         if (__builtin_amdgcn_ballot_w64(mrow > m + C::TH) != 0) {  // rare after the first tiles
             mask_fence();
@@ -331,7 +318,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
         const float nm = m == -INFINITY ? 0.f : -m;
         float rs[4] = {0.f, 0.f, 0.f, 0.f};  // four independent add chains instead of one 32-deep one
 #pragma unroll
-        for (int b = 0; b < C::NB; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const float p = fast_exp2(__builtin_fmaf(s[b][j], c2, nm));
@@ -342,21 +329,21 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
         l += sum_xchg32((rs[0] + rs[1]) + (rs[2] + rs[3]));
         if constexpr (DROP) {  // normaliser uses every p; only the P.V product sees the dropped ones
 #pragma unroll
-            for (int b = 0; b < C::NB; ++b)
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (!drop_keep(drow, k0s + kt + 32 * b + 4 * h + crow(j), a.drop_thr)) s[b][j] = 0.f;
         }
-        bf16x8 pf[C::NB][2];
+        bf16x8 pf[2][2];
 #pragma unroll
-        for (int b = 0; b < C::NB; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) pf[b][ss] = pack_acc_t<F16>(s[b], ss);
         {
 #pragma unroll
             for (int t = 0; t < C::NT; ++t)
 #pragma unroll
-                for (int b = 0; b < C::NB; ++b)
+                for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int ss = 0; ss < 2; ++ss) {
                         const int kb = (32 * b + 16 * ss) * D * 2;
@@ -365,7 +352,7 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
                         o[t] = mma<F16>(__builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7)), pf[b][ss], o[t]);
                     }
 #pragma unroll
-            for (int i = 0; i < 2 * C::NB * C::NT; ++i) {
+            for (int i = 0; i < 4 * C::NT; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);  // 2 x ds_read_b64_tr_b16
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
             }
@@ -410,12 +397,11 @@ __global__ __launch_bounds__(64 * NW, (NW == 6 ? 3 : 2)) void fa_fwd_v2_kernel(F
 template <bool F16, bool DROP>
 static void launch_fwd(const FwdArgs& a, int D, int max_q, hipStream_t st) {
     if (D == 128 || D == 64) {
-        constexpr int NW = SA_FWD_NW, KT = SA_FWD_KT;
-        constexpr int BM = FwdV2<128, NW, KT>::BM;
+        constexpr int NW = SA_FWD_NW;
+        constexpr int BM = FwdV2<128, NW>::BM;
         dim3 grid = attn_grid(a.Hq, a.nseg, (max_q + BM - 1) / BM), block(64 * NW);
-        if (D == 128)
-            hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, NW, KT>), grid, block, (4 * FwdV2<128, NW, KT>::TILE), st, a);
-        else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, NW, KT>), grid, block, (4 * FwdV2<64, NW, KT>::TILE), st, a);
+        if (D == 128) hipLaunchKernelGGL((fa_fwd_v2_kernel<128, F16, DROP, NW>), grid, block, (4 * FwdV2<128, NW>::TILE), st, a);
+        else hipLaunchKernelGGL((fa_fwd_v2_kernel<64, F16, DROP, NW>), grid, block, (4 * FwdV2<64, NW>::TILE), st, a);
         return;
     }
     dim3 grid((max_q + 127) / 128, a.Hq, a.nseg), block(256);

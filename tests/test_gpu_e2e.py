@@ -274,9 +274,11 @@ def test_gpu_shard_proxy_emulated_comm():
     loss (the emulation moves no data the model reads) and takes longer than the stub run.  The link efficiency is set
     so low (SCALING_AMD_PROXY_COMM_EFF) that every TP collective of this small model holds its CUs for ~10-20 ms: the
     step must grow by at least the blocking ones' sum, which small-model timing noise cannot hide."""
-    stub = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8"])
+    # two untimed warm-up steps: the first step's one-time costs (~2 s: library and kernel loading) swamp a 3-step mean
+    warm = ["--steps", "4", "--warmup", "2"]
+    stub = _bench_loss({}, ["--shard-proxy", "baseline3", "--micro-batch", "8", *warm])
     emu = _bench_loss({"SCALING_AMD_PROXY_COMM_EFF": "0.00065"},
-                      ["--shard-proxy", "baseline3", "--micro-batch", "8", "--proxy-comm", "emulate"])
+                      ["--shard-proxy", "baseline3", "--micro-batch", "8", "--proxy-comm", "emulate", *warm])
     assert emu["proxy_comm"] == "emulate" and stub["proxy_comm"] == "stub"
     assert emu["loss"] == stub["loss"]
     assert emu["per_rank_ms_per_step"][0] > stub["per_rank_ms_per_step"][0] + 100.0, (emu, stub)
