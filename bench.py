@@ -544,13 +544,24 @@ def _worker(a: argparse.Namespace) -> None:
         step()
     dist.barrier()
     sync()
+    prof_out = os.environ.get("SCALING_AMD_BENCH_CPROFILE")  # host-side profile of the timed steps only (rank 0)
+    prof = None
+    if prof_out and rank == 0:
+        import cProfile
+
+        prof = cProfile.Profile()
     t0 = time.perf_counter()
     per_step = []
     last: Optional[Any] = None
+    if prof is not None:
+        prof.enable()
     for _ in range(a.steps):
         s0 = time.perf_counter()
         last = step()
         per_step.append(time.perf_counter() - s0)
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(prof_out)
     dist.barrier()
     sync()
     mine = time.perf_counter() - t0

@@ -246,25 +246,27 @@ class _RopeFlashAttn(torch.autograd.Function):
         return o
 
     @staticmethod
-    def bwd_into(ctx: Any, do: torch.Tensor, dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor) -> None:
+    def bwd_into(saved: tuple, cfg: tuple, do: torch.Tensor, dq: torch.Tensor, dk: torch.Tensor, dv: torch.Tensor) -> None:
         """The attention backward written into the q/k/v slices (dq, dk, dv) of a dQKV buffer, the inverse rotation of
-        dq / dk folded into the dQ / dK epilogues.  (A separate method so race forensics can wrap it from outside the
-        production code: tools/attn_forensics.py.)"""
-        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
-        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
+        dq / dk folded into the dQ / dK epilogues.  ``saved`` is the node's ``ctx.saved_tensors``, unpacked ONCE by the
+        caller (under non-reentrant activation checkpointing a second unpack raises).  (A separate method so race
+        forensics can wrap it from outside the production code: tools/attn_forensics.py.)"""
+        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = saved
+        specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = cfg
         v = _view(base, specs[2])
         ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
                      local_heads, cos, sin, pos, rot_dim, seq_len, interleaved)
 
     @staticmethod
     def backward(ctx: Any, do: torch.Tensor):  # type: ignore[override]
-        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = saved
         _probe_record("rope_flash.saved@bwd", base, q, k, o, lse, pos, cos, sin, cu_q)
         _probe_record("rope_flash.do", do)
         specs = ctx.cfg[0]
         dbase = torch.empty_like(base)
         dq, dk, dv = (_view(dbase, sp) for sp in specs)
-        _RopeFlashAttn.bwd_into(ctx, do, dq, dk, dv)
+        _RopeFlashAttn.bwd_into(saved, ctx.cfg, do, dq, dk, dv)
         _probe_record("rope_flash.dbase", dbase)
         return (dbase,) + (None,) * 17
 

@@ -32,13 +32,13 @@ _NOROPE = os.environ.get("ATTN_FORENSICS_NOROPE") == "1"
 _orig_rope = attention._RopeFlashAttn.bwd_into
 
 
-def _orig(ctx, do, dq, dk, dv) -> None:
+def _orig(saved, cfg, do, dq, dk, dv) -> None:
     if not _NOROPE:
-        return _orig_rope(ctx, do, dq, dk, dv)
+        return _orig_rope(saved, cfg, do, dq, dk, dv)
     from scaling_amd.ops._ext import ext
 
-    base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = ctx.saved_tensors
-    specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = ctx.cfg
+    base, q, k, o, lse, cu_q, cu_k, cos, sin, pos = saved
+    specs, rot_dim, seq_len, interleaved, max_q, max_k, scale, causal, window, p_drop, seed, local_heads = cfg
     v = attention._view(base, specs[2])
     ext().fa_bwd(do, q, k, v, o, lse, cu_q, cu_k, max_q, max_k, scale, causal, window, dq, dk, dv, p_drop, seed,
                  local_heads)
@@ -88,22 +88,22 @@ def _mismatch(dbase: torch.Tensor, d2: torch.Tensor, d3: torch.Tensor, views1, v
                       cols, vals])
 
 
-def bwd_into(ctx, do, dq, dk, dv) -> None:
+def bwd_into(saved, cfg, do, dq, dk, dv) -> None:
     if _SYNC and do.is_cuda:
         torch.cuda.synchronize(do.device)
-    _orig(ctx, do, dq, dk, dv)
+    _orig(saved, cfg, do, dq, dk, dv)
     if _SYNC and do.is_cuda:
         torch.cuda.synchronize(do.device)
     if not _TWICE:
         return
-    base = ctx.saved_tensors[0]
-    specs = ctx.cfg[0]
+    base = saved[0]
+    specs = cfg[0]
     dbase = dq.as_strided(base.shape, base.stride(), dq.storage_offset() - specs[0][2])
     outs = []
     for _ in range(2):
         d = torch.empty_like(base)
         views = [attention._view(d, sp) for sp in specs]
-        _orig(ctx, do, *views)
+        _orig(saved, cfg, do, *views)
         outs.append((d, views))
     (d2, v2), (d3, _) = outs
     rec = _mismatch(dbase, d2, d3, (dq, dk, dv), v2)
