@@ -135,7 +135,8 @@ PRESETS: dict[str, dict[str, Any]] = {
     "baseline3": {"tp": 2, "pp": 1, "micro_batch": 8, "grad_acc": 1, "sequence_parallel": True, "tp_comm_chunks": 0,
                   "activation_checkpointing": "disabled", "lora": False, "zero": 1},
     # "TP=2 PP=2 DP=2 (full 3D parallel, 1F1B pipeline) with activation checkpointing": the reference's per-layer
-    # checkpointing (every_layer).  Micro-batching: see profiles/proxy_baseline4_mb_r6.md
+    # checkpointing (every_layer).  Micro-batching 4 x 4: per-stage proxy with emulated comm, bubble applied, 2041 ms vs
+    # 2058 (2 x 8) and 2080 (1 x 16) -- profiles/proxy_baseline4_mb_r6.md
     "baseline4": {"tp": 2, "pp": 2, "micro_batch": 4, "grad_acc": 4, "sequence_parallel": True, "tp_comm_chunks": 0,
                   "activation_checkpointing": "every_layer", "lora": False, "zero": 1},
     # the same layout with this framework's selective recompute (every_layer_save_matmuls keeps every GEMM output, the

