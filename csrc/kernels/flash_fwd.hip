@@ -194,6 +194,8 @@ struct FwdV2 {
 // their code is in git history before commit "Delete losing attention variants".  128-key tiles (8 waves x 32 queries,
 // 128 KiB of LDS, one workgroup per CU, causal tiles past a wave's queries skipped): 1.28 vs 1.13 ms at the 7B shape,
 // profiles/attn_fwd_kt128_ab_r6.log (code in git history, commit "Drop the race-forensics build switches").
+// K / V staged through registers (buffer loads issued before a tile's MFMAs, ds_write after them, T14) instead of
+// LDS-DMA: 1.22-1.26 vs 1.13-1.16 ms, profiles/attn_fwd_regstage_ab_r6.log.
 // NW = 4: 2 workgroups / CU = 2 waves / SIMD; NW = 6 (BM = 192): 2 workgroups / CU = 3 waves / SIMD (<= 168 VGPRs)
 #ifndef SA_FWD_NW
 #define SA_FWD_NW 4
