@@ -771,7 +771,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
     m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
     m.def("embed_fwd", &embed_fwd, "vocab-parallel embedding forward");
-    m.def("embed_bwd", &embed_bwd, "deterministic embedding backward");
+    // (waits for the device: unique_consecutive reads its count back) -- without the GIL, so a thread that blocks here
+    // never stalls the Python threads it waits for (the asynchronous rehearsal's collectives deadlocked on it)
+    m.def("embed_bwd", &embed_bwd, "deterministic embedding backward", py::call_guard<py::gil_scoped_release>());
     m.def("adamw_", &adamw_, "fused AdamW on flat fp32 buffers");
     m.def("sumsq_", &sumsq_, "sum of squares + non-finite count");
     m.def("cast_scale_", &cast_scale_, "y = cast(x * scale)");

@@ -118,6 +118,9 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         # read and its output written when the stream gets there / the peers are done
         (["--gpus", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
         (["--gpus", "4", "--grad-acc", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1", "SCALING_AMD_COMM_DELAY_US": "1000"}),
+        # TP2 + SP with the row-parallel GEMMs in 4 pieces on the TP communication stream, async input-gradient
+        # all-reduce
+        (["--gpus", "2", "--tp", "2", "--sequence-parallel", "--tp-comm-chunks", "4"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):
