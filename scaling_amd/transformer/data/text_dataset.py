@@ -173,6 +173,9 @@ class TextDataset(BaseDataset[TextDatasetItem, TextDatasetBatchBeforeSync, TextD
         if topology is None:
             assert batch is not None
             return TextDatasetBatch(input_token_ids=batch.token_ids[:, :-1], target_token_ids=batch.token_ids[:, 1:])
+        if (topology.config.model_parallel_size == 1 and batch is not None and not batch.token_ids.is_cuda
+                and topology.device.type == "cuda"):
+            return TextDataset._host_derived_batch(batch.token_ids, topology.device)
         if topology.model_parallel_rank == 0:
             assert batch is not None
             tensors: list[Optional[torch.Tensor]] = [batch.token_ids]
@@ -181,6 +184,24 @@ class TextDataset(BaseDataset[TextDatasetItem, TextDatasetBatchBeforeSync, TextD
             tensors = [None]
         tok = broadcast_data(tensors=tensors, dtype=torch.long, topology=topology)[0]
         return TextDatasetBatch(input_token_ids=tok[:, :-1], target_token_ids=tok[:, 1:])
+
+    @staticmethod
+    def _host_derived_batch(token_ids: torch.Tensor, device: torch.device) -> TextDatasetBatch:
+        """TP 1 with the batch still on the host: cu_seqlens (plain and -1 padded) and position ids are derived from
+        the host copy of the token ids and travel with them as asynchronous pinned copies -- on the device they cost
+        ~40 small kernels and a device sync (``torch.nonzero``) per micro-batch, which a small model's host-bound step
+        pays in full.  The values are those of ``TextDatasetBatch``'s own derivation (same functions)."""
+        from .utils import add_cumulative_seq_lengths_padding, get_cumulative_seq_lengths, get_position_ids
+
+        inp = token_ids[:, :-1]
+        b, s = inp.shape
+        cu = get_cumulative_seq_lengths(inp)
+        host = {"tok": token_ids, "cu": cu, "cu_pad": add_cumulative_seq_lengths_padding(cu, b * (s + 1)),
+                "pos": get_position_ids(inp)}
+        dev = {k: (v if v.is_pinned() else v.pin_memory()).to(device, non_blocking=True) for k, v in host.items()}
+        tok = dev["tok"]
+        return TextDatasetBatch(input_token_ids=tok[:, :-1], target_token_ids=tok[:, 1:], position_ids=dev["pos"],
+                                cumulative_seq_lengths=dev["cu"], cumulative_seq_lengths_padded=dev["cu_pad"])
 
     @staticmethod
     def jsonl_to_memory_map(data_file_jsonl: Path, prefix_path_memory_map: Path) -> None:

@@ -297,3 +297,28 @@ def test_gpu_shard_proxy_tp_chunks_match():
         assert np.isfinite(cfg["loss"]) and all(np.isfinite(v) for v in cfg["param_checksum"])
     assert abs(losses["2"] - losses["1"]) < 1e-3 * abs(losses["1"]), losses
     assert abs(losses["4"] - losses["1"]) < 1e-3 * abs(losses["1"]), losses
+
+
+def test_gpu_host_derived_batch_matches_device_derivation():
+    """TP 1 with the batch on the host: ``TextDataset.sync_batch_to_model_parallel`` derives cu_seqlens (plain and
+    -1 padded) and position ids from the host copy (no device sync, no small kernels) -- the same values as
+    ``TextDatasetBatch`` derives from the device tensors, including EOD resets."""
+    from types import SimpleNamespace
+
+    from scaling_amd.transformer.data.text_dataset import TextDataset
+    from scaling_amd.transformer.data.text_dataset_batch import TextDatasetBatch
+
+    torch.manual_seed(0)
+    tok = torch.randint(0, 6, (3, 65))  # token 0 = EOD: several segments per row
+    topo = SimpleNamespace(config=SimpleNamespace(model_parallel_size=1), device=torch.device("cuda", 0),
+                           model_parallel_rank=0)
+    from scaling_amd.transformer.data.text_dataset_batch import TextDatasetBatchBeforeSync
+
+    host = TextDataset.sync_batch_to_model_parallel(topo, TextDatasetBatchBeforeSync(token_ids=tok))
+    g = tok.cuda()
+    ref = TextDatasetBatch(input_token_ids=g[:, :-1], target_token_ids=g[:, 1:])
+    torch.cuda.synchronize()
+    for name in ("input_token_ids", "target_token_ids", "cumulative_seq_lengths", "cumulative_seq_lengths_padded",
+                 "position_ids", "loss_weights"):
+        a, b = getattr(host, name), getattr(ref, name)
+        assert a.is_cuda and a.dtype == b.dtype and torch.equal(a, b), name
