@@ -87,6 +87,19 @@ def _to_python(x: Any) -> Any:
     return x
 
 
+def _loss_and_metrics_to_python(loss: torch.Tensor, metrics: Any) -> tuple[float, Any]:
+    """The step's loss and its scalar metrics read back in ONE device-to-host copy (one sync instead of one per value);
+    non-scalar or non-tensor metrics go through ``_to_python``."""
+    if isinstance(metrics, dict):
+        keys = [k for k, v in metrics.items() if torch.is_tensor(v) and v.numel() == 1 and v.device == loss.device]
+        if keys:
+            vals = torch.stack([loss.detach().reshape(()).double()] +
+                               [metrics[k].detach().reshape(()).double() for k in keys]).tolist()
+            out = {k: (vals[1 + keys.index(k)] if k in keys else _to_python(v)) for k, v in metrics.items()}
+            return float(vals[0]), out
+    return float(loss.detach().cpu().item()), _to_python(metrics)
+
+
 class _StepTimer:
     """Step duration from HIP events on the compute stream (no device-wide synchronize).
 
@@ -255,7 +268,7 @@ class ParallelModule(PipePartitionedModule, Generic[BaseLossInputGeneric, BaseDa
                 self.communicator_loss_out.send_data(data, topo.get_global_rank(pipe_parallel_rank=0))
             return None, None
         assert data is not None
-        return float(data[0].cpu().item()), _to_python(data[1])
+        return _loss_and_metrics_to_python(data[0], data[1])
 
     # ------------------------------------------------------------------ steps
     def train_step(self, dataloader: Any, optimizer: BaseOptimizer, sync_batch_to_model_parallel: Callable,
