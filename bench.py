@@ -125,6 +125,10 @@ def apply_example(a: argparse.Namespace, argv: Optional[list[str]] = None) -> ar
         a.grad_acc = t["gradient_accumulation_steps"]
     if "seq_len" not in given:
         a.seq_len = example_config()["transformer_architecture"]["sequence_length"]
+    if "gemm_tuning" not in given:
+        # the TunableOp table holds the 7B shapes only: for this model "use" is a per-GEMM lookup miss (~20 us of host
+        # time each in a host-bound step), 4.7 vs 4.4 ms/step (profiles/bench_ab_ex_tuning_r6.log)
+        a.gemm_tuning = "off"
     return a
 
 
