@@ -238,3 +238,18 @@ def test_bench_launcher_cu_split(monkeypatch, split, gpus, backend, ndev, want):
     a = argparse.Namespace(gpus=gpus, backend=backend, launch_timeout=10)
     assert bench._launch(a) == 0
     assert [e.get("HSA_CU_MASK") for e in envs] == want
+
+
+def test_bench_transformer_example_args():
+    """``--model transformer_example`` (BASELINE #2) takes the example config's micro-batching and sequence length and
+    turns the 7B TunableOp table off; explicit flags win."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cfg = bench.example_config()
+    a = bench._args(["--model", "transformer_example"])
+    assert a.micro_batch == cfg["topology"]["micro_batch_size"]
+    assert a.grad_acc == cfg["topology"]["gradient_accumulation_steps"]
+    assert a.seq_len == cfg["transformer_architecture"]["sequence_length"] and a.gemm_tuning == "off"
+    b = bench._args(["--model", "transformer_example", "--seq-len", "32", "--gemm-tuning", "use"])
+    assert b.seq_len == 32 and b.gemm_tuning == "use"
