@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <deque>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -167,6 +168,74 @@ void rw_collective(int64_t kind, const c10::intrusive_ptr<c10d::ProcessGroup>& p
     });
 }
 
+// Pipeline p2p (the framework's batched isend / irecv).  A send job waits for `event` (the payload's copy-out),
+// POSTS the gloo sends and returns without waiting for them (a send completes when the peer receives, which may be a
+// later job of the peer's worker -- as an RCCL send runs on its own stream); their works are kept under `send_id` for
+// rw_send_wait.  A receive job posts its receives, waits for them, and opens gate (base, idx) at `gen`.
+// peers are group ranks of `pg`.
+static std::mutex g_sends_m;
+static std::map<int64_t, std::vector<c10::intrusive_ptr<c10d::Work>>> g_sends;
+
+void rw_p2p_send(const c10::intrusive_ptr<c10d::ProcessGroup>& pg, std::vector<at::Tensor> hs, std::vector<int64_t> peers,
+                 std::vector<int64_t> tags, int64_t event, int64_t send_id) {
+    worker().push([=]() {
+        trace("start send", send_id, 4);
+        try {
+            if (event != 0)
+                TORCH_CHECK(hipEventSynchronize(reinterpret_cast<hipEvent_t>((uintptr_t)event)) == hipSuccess,
+                            "rehearsal worker: hipEventSynchronize");
+            std::vector<c10::intrusive_ptr<c10d::Work>> works;
+            for (size_t i = 0; i < hs.size(); ++i) {
+                std::vector<at::Tensor> v{hs[i]};
+                works.push_back(pg->send(v, (int)peers[i], (int)tags[i]));
+            }
+            std::lock_guard<std::mutex> lk(g_sends_m);
+            g_sends[send_id] = std::move(works);
+        } catch (const std::exception& e) {
+            fail(e.what());
+        } catch (...) {
+            fail("rehearsal worker: unknown error");
+        }
+        trace("sends posted", send_id, 4);
+    });
+}
+
+void rw_p2p_recv(const c10::intrusive_ptr<c10d::ProcessGroup>& pg, std::vector<at::Tensor> hs, std::vector<int64_t> peers,
+                 std::vector<int64_t> tags, int64_t base, int64_t idx, int64_t gen) {
+    worker().push([=]() {
+        trace("start recv", idx, 5);
+        try {
+            std::vector<c10::intrusive_ptr<c10d::Work>> works;
+            for (size_t i = 0; i < hs.size(); ++i) {
+                std::vector<at::Tensor> v{hs[i]};
+                works.push_back(pg->recv(v, (int)peers[i], (int)tags[i]));
+            }
+            for (auto& w : works) w->wait();
+        } catch (const std::exception& e) {
+            fail(e.what());
+        } catch (...) {
+            fail("rehearsal worker: unknown error");
+        }
+        trace("received", idx, 5);
+        open_gate(base, idx, gen);
+    });
+}
+
+// Waits (GIL released) until the sends of `send_id` have completed, in program order (called inside a host turn, so
+// the worker has posted them).
+void rw_send_wait(int64_t send_id) {
+    std::vector<c10::intrusive_ptr<c10d::Work>> works;
+    {
+        std::lock_guard<std::mutex> lk(g_sends_m);
+        auto it = g_sends.find(send_id);
+        if (it == g_sends.end()) return;  // failed job (its error is raised by rw_check)
+        works = std::move(it->second);
+        g_sends.erase(it);
+    }
+    pybind11::gil_scoped_release no_gil;
+    for (auto& w : works) w->wait();
+}
+
 // Python-level gloo call in program order: host_begin blocks (GIL released) until every earlier job has run and the
 // worker waits for host_end.
 int64_t rw_host_begin() {
@@ -216,4 +285,9 @@ void register_rehearsal(pybind11::module& m) {
     m.def("rw_host_end", &rw_host_end, "rehearsal worker: a Python-level gloo call is done");
     m.def("rw_check", &rw_check, "rehearsal worker: raise the first failed job's error");
     m.def("rw_drain", &rw_drain, "rehearsal worker: wait for every queued job");
+    m.def("rw_p2p_send", &rw_p2p_send, "rehearsal worker: queue posting pipeline sends behind an event",
+          pybind11::call_guard<pybind11::gil_scoped_release>());
+    m.def("rw_p2p_recv", &rw_p2p_recv, "rehearsal worker: queue pipeline receives behind a stream gate",
+          pybind11::call_guard<pybind11::gil_scoped_release>());
+    m.def("rw_send_wait", &rw_send_wait, "rehearsal worker: wait for a send batch (inside a host turn)");
 }

@@ -155,7 +155,11 @@ class PipeCommunicator:
 
     @property
     def _host_staged(self) -> bool:
-        return self.local_device.type == "cuda" and dist.get_backend() == "gloo"
+        # (the asynchronous rehearsal routes GPU p2p through its own stream-ordered staging: core/topology/gloo_gpu.py)
+        from ...topology import gloo_gpu
+
+        return (self.local_device.type == "cuda" and dist.get_backend() == "gloo"
+                and not (gloo_gpu.installed() and gloo_gpu.async_mode()))
 
     @property
     def _wire_device(self) -> torch.device:

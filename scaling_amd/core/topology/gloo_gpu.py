@@ -25,8 +25,9 @@ order follows message arrival).  Two modes:
   order): it waits until the stream has copied the input out, runs gloo on the host copies, writes the result, and
   opens the gate.  So the input is read when the STREAM gets there, long after the call returned, and the output lands
   when the peers are done -- a missing ``record_stream`` / early free / missing stream wait in this framework changes
-  the result, which the race check's multi- vs single-stream comparison then shows.  Pipeline p2p is refused in this
-  mode (its host staging, ``communicator._HostStagedWork``, is synchronous).
+  the result, which the race check's multi- vs single-stream comparison then shows.  Pipeline p2p goes the same way
+  (``_async_batch_p2p``): a send's payload is copied out when the stream gets there and the worker posts the gloo
+  send behind that copy without waiting for it; a receive lands through a gate.
 
 Only the rehearsal installs this; with RCCL (``nccl``) or CPU gloo nothing is wrapped.
 """
@@ -340,9 +341,76 @@ def _wrap_host_only(orig: Callable[..., Any]) -> Callable[..., Any]:
     return fn
 
 
-def _refuse_p2p(*_a: Any, **_k: Any) -> Any:
-    raise RuntimeError("SCALING_AMD_REHEARSAL_ASYNC=1 does not support pipeline p2p (its host staging is synchronous); "
-                       "run pipeline layouts in the synchronous rehearsal")
+class _AsyncSendWork:
+    """Handle of a queued send batch: ``wait`` returns once gloo completed the sends, in program order among the
+    worker's jobs (a host turn); the payload copies stay alive until then."""
+
+    def __init__(self, send_id: int, keep: tuple) -> None:
+        self.send_id, self.keep = send_id, keep
+
+    def wait(self, timeout: Any = None) -> bool:
+        if self.keep is not None:
+            from ...ops._ext import ext
+
+            _host_call(lambda: ext().rw_send_wait(self.send_id))
+            self.keep = None
+        return True
+
+    def is_completed(self) -> bool:
+        return self.keep is None
+
+
+def _async_batch_p2p(ops: list) -> list:
+    """``batch_isend_irecv`` with RCCL's lifetimes: each send's payload is copied out when the current stream gets
+    there and the worker posts the gloo sends behind that copy; receives land through a stream gate.  One handle for
+    the sends, one for the receives (``wait``: the current stream waits for the received data)."""
+    from ...ops._ext import ext
+
+    ext().rw_check()
+    if "gates" not in _state:
+        _state["gates"] = _Gates()
+    _retire_pinned()
+    works: list = []
+    dev = ops[0].tensor.device
+    cur = torch.cuda.current_stream(dev)
+
+    def peer(op: Any) -> int:
+        return dist.get_group_rank(op.group, op.peer) if op.group is not None else op.peer
+
+    for kind in ("send", "recv"):
+        sel = [op for op in ops if (op.op is dist.isend) == (kind == "send")]
+        if not sel:
+            continue
+        groups = {id(op.group) for op in sel}
+        assert len(groups) == 1, "asynchronous rehearsal: one process group per p2p batch"
+        pg = _pg(sel[0].group)
+        hs = [torch.empty(op.tensor.shape, dtype=op.tensor.dtype, pin_memory=True) for op in sel]
+        peers, tags = [peer(op) for op in sel], [int(op.tag or 0) for op in sel]
+        if kind == "send":
+            with torch.cuda.stream(cur):
+                for h, op in zip(hs, sel):
+                    h.copy_(op.tensor, non_blocking=True)  # read when the stream gets here
+                e_in = torch.cuda.Event()
+                e_in.record(cur)
+            sid = _state.get("send_id", 0)
+            _state["send_id"] = sid + 1
+            _trace(f"send batch {sid}: {[tuple(op.tensor.shape) for op in sel]} -> {peers}")
+            ext().rw_p2p_send(pg, hs, peers, tags, e_in.cuda_event, sid)
+            works.append(_AsyncSendWork(sid, (hs, e_in, [op.tensor for op in sel])))
+        else:
+            gates = _state["gates"]
+            idx, gen = gates.take()
+            with torch.cuda.stream(cur):
+                ext().gate_stream_wait(gates.base, idx, gen)
+                for h, op in zip(hs, sel):
+                    op.tensor.copy_(h, non_blocking=True)  # written once the peers' data arrived
+                e_out = torch.cuda.Event()
+                e_out.record(cur)
+            _state.setdefault("pinned", []).append((e_out, None, hs, None))
+            _trace(f"recv batch gate {idx}/{gen}: {[tuple(op.tensor.shape) for op in sel]} <- {peers}")
+            ext().rw_p2p_recv(pg, hs, peers, tags, gates.base, idx, gen)
+            works.append(_AsyncWork(e_out, tuple(op.tensor for op in sel)))
+    return works
 
 
 def install() -> None:
@@ -372,7 +440,7 @@ def install() -> None:
             return _orig["destroy_process_group"](*a, **k)
 
         dist.destroy_process_group = destroy
-        dist.batch_isend_irecv = _refuse_p2p
+        dist.batch_isend_irecv = _async_batch_p2p
 
 
 def installed() -> bool:

@@ -119,3 +119,56 @@ def test_async_mode_worker_orders_jobs_and_host_calls():
         assert torch.equal(torch.tensor(g), torch.cat(xs))
         assert torch.equal(torch.tensor(m), torch.maximum(xs[0], xs[1]))
         assert ranks == list(range(world)) and flags == [1] * 22
+
+
+def _async_p2p_worker(rank: int, world: int, port: int, q) -> None:
+    """Asynchronous rehearsal p2p, host side: send jobs POST their gloo sends without waiting (both ranks send first,
+    then receive -- a worker that waited for its sends would deadlock here), receive jobs open their gate once the data
+    arrived, and ``rw_send_wait`` inside a host turn retires a send batch."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from scaling_amd.ops._ext import ext
+
+    pg = dist.distributed_c10d._get_default_group()
+    flags = torch.zeros(8, dtype=torch.int32)
+    peer = 1 - rank
+    outs = []
+    for i in range(3):
+        payload = [torch.full((5,), float(10 * rank + i)), torch.arange(3, dtype=torch.int64) + rank]
+        ext().rw_p2p_send(pg, payload, [peer, peer], [0, 0], 0, i)
+        got = [torch.empty(5), torch.empty(3, dtype=torch.int64)]
+        ext().rw_p2p_recv(pg, got, [peer, peer], [0, 0], flags.data_ptr(), i, 1)
+        outs.append(got)
+    t = ext().rw_host_begin()
+    for i in range(3):
+        ext().rw_send_wait(i)
+    ext().rw_host_end(t)
+    ext().rw_drain()
+    ext().rw_check()
+    t0 = time.time()
+    while int(flags[:3].min()) < 1 and time.time() - t0 < 30:
+        time.sleep(0.01)
+    q.put((rank, [[a.tolist(), b.tolist()] for a, b in outs], flags[:3].tolist()))
+    dist.destroy_process_group()
+
+
+def test_async_mode_worker_p2p_posts_sends():
+    world = 2
+    port = find_free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_async_p2p_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in ps))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in range(world):
+        outs, flags = res[r]
+        peer = 1 - r
+        assert flags == [1, 1, 1]
+        for i, (a, b) in enumerate(outs):
+            assert a == [float(10 * peer + i)] * 5 and b == [peer, peer + 1, peer + 2]

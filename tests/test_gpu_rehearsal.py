@@ -121,6 +121,8 @@ def test_rehearsal_train_resume_bit_exact_gpu(tmp_path, mp, pp, world):
         # TP2 + SP with the row-parallel GEMMs in 4 pieces on the TP communication stream, async input-gradient
         # all-reduce
         (["--gpus", "2", "--tp", "2", "--sequence-parallel", "--tp-comm-chunks", "4"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
+        # TP2 x PP2: pipeline p2p with RCCL's lifetimes too (payload read when the stream gets there, sends in flight)
+        (["--gpus", "4", "--tp", "2", "--pp", "2", "--grad-acc", "2"], {"SCALING_AMD_REHEARSAL_ASYNC": "1"}),
     ],
 )
 def test_race_check_multi_stream_equals_single_stream(args, env):
