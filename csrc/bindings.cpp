@@ -687,14 +687,11 @@ void spin_us(int64_t us) { sa_launch::spin(us, cur_stream()); }
 // ---- stream gates (asynchronous rehearsal collectives, core/topology/gloo_gpu.py): a stream waits in the command
 // processor (hipStreamWaitValue32, no CU spins) until the host writes a generation number into a flag word.
 // kind 0: hipMallocSignalMemory words; kind 1: coherent pinned host memory.  Returns the base address.
-int64_t gate_flags_alloc(int64_t n, int64_t kind) {
+// flag words in coherent, device-mapped host memory (hipMallocSignalMemory was refused on the pool's boxes)
+int64_t gate_flags_alloc(int64_t n) {
     void* p = nullptr;
     const size_t bytes = (size_t)std::max<int64_t>(n, 1) * sizeof(uint32_t);
-    if (kind == 0) {
-        TORCH_CHECK(hipExtMallocWithFlags(&p, bytes, hipMallocSignalMemory) == hipSuccess, "gate: signal memory");
-    } else {
-        TORCH_CHECK(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess, "gate: pinned memory");
-    }
+    TORCH_CHECK(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess, "gate: pinned memory");
     std::memset(p, 0, bytes);
     return (int64_t)(uintptr_t)p;
 }
@@ -782,7 +779,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("act_fwd", &act_fwd, "activation forward (0 gelu, 1 silu, 2 gelu-tanh)");
     m.def("act_bwd", &act_bwd, "activation backward");
     m.def("spin_us", &spin_us, "debug: busy-wait kernel of ~us microseconds on the current stream");
-    m.def("gate_flags_alloc", &gate_flags_alloc, "stream gates: n flag words (kind 0 signal memory, 1 pinned host)");
+    m.def("gate_flags_alloc", &gate_flags_alloc, "stream gates: n flag words (coherent pinned host memory)");
     m.def("gate_flag_write", &gate_flag_write, "stream gates: host store of a flag word (after a full fence)");
     m.def("gate_flag_read", &gate_flag_read, "stream gates: host load of a flag word");
     m.def("gate_stream_wait", &gate_stream_wait, "stream gates: the current stream waits until flag[idx] >= value");

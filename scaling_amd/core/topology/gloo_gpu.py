@@ -130,8 +130,7 @@ class _Gates:
     def __init__(self, n: int = 1 << 14) -> None:
         from ...ops._ext import ext
 
-        kind = int(os.environ.get("SCALING_AMD_REHEARSAL_GATE_KIND", "1"))  # 1: coherent pinned host memory
-        self.base = ext().gate_flags_alloc(n, kind)
+        self.base = ext().gate_flags_alloc(n)  # coherent pinned host memory
         self.n, self.i = n, 0
         self.gen = [0] * n
 

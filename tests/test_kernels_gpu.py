@@ -1021,3 +1021,33 @@ def test_xgmi_emulate_moves_bytes_and_holds_time():
         ext().xgmi_emulate(src, scratch, 1024, 2000.0, 4)  # 2 ms each
     torch.cuda.synchronize()
     assert time.perf_counter() - t0 >= 0.0095
+
+
+def test_stream_gate_holds_until_host_flag():
+    """The asynchronous rehearsal's stream gate (``ext().gate_stream_wait``: hipStreamWaitValue32 on a flag word in
+    coherent pinned host memory): work queued behind the gate runs only after the host writes the flag, and a later
+    gate on the same word at the next generation releases at once when the flag is written first."""
+    import threading
+    import time
+
+    x = torch.zeros(1, device="cuda")
+    s = torch.cuda.Stream()
+    base = ext().gate_flags_alloc(4)
+    ev = torch.cuda.Event()
+    with torch.cuda.stream(s):
+        x.fill_(1)
+        ext().gate_stream_wait(base, 0, 1)
+        x.add_(1)
+        ev.record(s)
+    t0 = time.time()
+    threading.Timer(0.3, lambda: ext().gate_flag_write(base, 0, 1)).start()
+    time.sleep(0.1)
+    assert not ev.query()  # held by the gate
+    s.synchronize()
+    assert time.time() - t0 >= 0.29 and x.item() == 2.0
+    ext().gate_flag_write(base, 0, 2)
+    with torch.cuda.stream(s):
+        ext().gate_stream_wait(base, 0, 2)
+        x.add_(1)
+    s.synchronize()
+    assert x.item() == 3.0 and ext().gate_flag_read(base, 0) == 2
