@@ -235,15 +235,10 @@ at::Tensor embed_bwd(const at::Tensor& dy, const at::Tensor& ids, int64_t num_ro
     auto sorted = at::sort(idc, /*stable=*/true, /*dim=*/0, /*descending=*/false);
     auto sid = std::get<0>(sorted).contiguous();
     auto order = std::get<1>(sorted).contiguous();
-    auto uc = at::unique_consecutive(sid, /*return_inverse=*/false, /*return_counts=*/true);
-    auto uniq = std::get<0>(uc).contiguous();
-    auto counts = std::get<2>(uc);
-    auto seg = at::zeros({uniq.numel() + 1}, idc.options());
-    seg.narrow(0, 1, uniq.numel()).copy_(at::cumsum(counts, 0));
     auto dW = at::zeros({num_rows, H}, dy.options());
     auto dyc = dy.contiguous();
-    sa_launch::embed_bwd(dt(dyc), dyc.data_ptr(), order.data_ptr<int64_t>(), seg.data_ptr<int64_t>(),
-                         uniq.data_ptr<int64_t>(), uniq.numel(), dW.data_ptr(), (int)H, v0, num_rows, cur_stream());
+    sa_launch::embed_bwd(dt(dyc), dyc.data_ptr(), order.data_ptr<int64_t>(), sid.data_ptr<int64_t>(), sid.numel(),
+                         dW.data_ptr(), (int)H, v0, num_rows, cur_stream());
     return dW;
 }
 
@@ -768,8 +763,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("xent_stats", &xent_stats, "cross-entropy row statistics");
     m.def("xent_bwd", &xent_bwd, "cross-entropy backward");
     m.def("embed_fwd", &embed_fwd, "vocab-parallel embedding forward");
-    // (waits for the device: unique_consecutive reads its count back) -- without the GIL, so a thread that blocks here
-    // never stalls the Python threads it waits for (the asynchronous rehearsal's collectives deadlocked on it)
+    // (the GIL released: an embedding backward that waited for the device here -- its former unique / count
+    // formulation -- while holding it deadlocked the asynchronous rehearsal's collectives)
     m.def("embed_bwd", &embed_bwd, "deterministic embedding backward", py::call_guard<py::gil_scoped_release>());
     m.def("adamw_", &adamw_, "fused AdamW on flat fp32 buffers");
     m.def("sumsq_", &sumsq_, "sum of squares + non-finite count");

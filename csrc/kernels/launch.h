@@ -40,8 +40,8 @@ void xent_bwd(int dtype, const void* logits, const int64_t* tgt, const float* ls
               int64_t rows, int V, int64_t v0, hipStream_t st);
 void embed_fwd(int dtype, const int64_t* ids, const void* W, void* out, int64_t ntok, int H, int64_t v0, int64_t Vp,
                hipStream_t st);
-void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* seg, const int64_t* seg_id, int64_t nseg,
-               void* dW, int H, int64_t v0, int64_t Vp, hipStream_t st);
+void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* sid, int64_t ntok, void* dW, int H,
+               int64_t v0, int64_t Vp, hipStream_t st);
 void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, void* pout, int64_t n, float lr,
            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale, hipStream_t st);
 int sumsq_blocks(int64_t n);

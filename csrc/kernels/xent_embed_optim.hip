@@ -115,22 +115,27 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
     }
 }
 
-// Deterministic backward: tokens pre-sorted by id (stable), segment [seg[k], seg[k+1]) shares id.
-// dW[id] = sum over the segment in sorted order (fp32 accumulate). Rows never hit stay as the caller
-// initialised them (zero).
+// dW[id] = sum of dy rows whose token is id, over the token positions sorted by id (stable, so the sum runs in token
+// order and the result is deterministic): one wave per sorted position; the wave at the first position of each id's
+// run adds the run's rows and writes the row.  Rows of ids outside this rank's shard are skipped; rows with no token
+// keep the caller's zeros.  Run boundaries are found on the device, so the host never reads the number of distinct
+// ids back (a device sync per backward in the unique / count formulation).
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const T* __restrict__ dy, const int64_t* __restrict__ order,
-                                                        const int64_t* __restrict__ seg, const int64_t* __restrict__ seg_id,
-                                                        int64_t nseg, T* __restrict__ dW, int H, int64_t v0, int64_t Vp) {
+                                                        const int64_t* __restrict__ sid, int64_t ntok, T* __restrict__ dW,
+                                                        int H, int64_t v0, int64_t Vp) {
     const int lane = threadIdx.x & 63;
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= nseg) return;
-    const int64_t id = seg_id[k] - v0;
+    if (k >= ntok) return;
+    const int64_t s = sid[k];
+    if (k > 0 && sid[k - 1] == s) return;  // not the first position of its run
+    const int64_t id = s - v0;
     if (id < 0 || id >= Vp) return;
-    const int64_t b = seg[k], e = seg[k + 1];
+    int64_t e = k + 1;
+    while (e < ntok && sid[e] == s) ++e;
     for (int c = lane * 8; c < H; c += 512) {
         float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int64_t r = b; r < e; ++r) {
+        for (int64_t r = k; r < e; ++r) {
             float v[8];
             V8<T>::ld(dy + order[r] * H + c, v);
 #pragma unroll
@@ -283,13 +288,13 @@ void embed_fwd(int dtype, const int64_t* ids, const void* W, void* out, int64_t 
     else if (dtype == DT_F16) hipLaunchKernelGGL(embed_fwd_kernel<f16>, g, 256, 0, st, ids, (const f16*)W, (f16*)out, ntok, H, v0, Vp);
     else hipLaunchKernelGGL(embed_fwd_kernel<float>, g, 256, 0, st, ids, (const float*)W, (float*)out, ntok, H, v0, Vp);
 }
-void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* seg, const int64_t* seg_id, int64_t nseg,
-               void* dW, int H, int64_t v0, int64_t Vp, hipStream_t st) {
-    if (nseg == 0) return;
-    const int g = (int)((nseg + 3) / 4);
-    if (dtype == DT_BF16) hipLaunchKernelGGL(embed_bwd_kernel<u16>, g, 256, 0, st, (const u16*)dy, order, seg, seg_id, nseg, (u16*)dW, H, v0, Vp);
-    else if (dtype == DT_F16) hipLaunchKernelGGL(embed_bwd_kernel<f16>, g, 256, 0, st, (const f16*)dy, order, seg, seg_id, nseg, (f16*)dW, H, v0, Vp);
-    else hipLaunchKernelGGL(embed_bwd_kernel<float>, g, 256, 0, st, (const float*)dy, order, seg, seg_id, nseg, (float*)dW, H, v0, Vp);
+void embed_bwd(int dtype, const void* dy, const int64_t* order, const int64_t* sid, int64_t ntok, void* dW, int H,
+               int64_t v0, int64_t Vp, hipStream_t st) {
+    if (ntok == 0) return;
+    const int g = (int)((ntok + 3) / 4);
+    if (dtype == DT_BF16) hipLaunchKernelGGL(embed_bwd_kernel<u16>, g, 256, 0, st, (const u16*)dy, order, sid, ntok, (u16*)dW, H, v0, Vp);
+    else if (dtype == DT_F16) hipLaunchKernelGGL(embed_bwd_kernel<f16>, g, 256, 0, st, (const f16*)dy, order, sid, ntok, (f16*)dW, H, v0, Vp);
+    else hipLaunchKernelGGL(embed_bwd_kernel<float>, g, 256, 0, st, (const float*)dy, order, sid, ntok, (float*)dW, H, v0, Vp);
 }
 void adamw(int gdtype, int pdtype, float* p, const void* g, float* m, float* v, void* pout, int64_t n, float lr,
            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt, float gscale, hipStream_t st) {

@@ -297,6 +297,25 @@ def test_embedding():
     assert torch.equal(g1, W.grad)
 
 
+def test_embedding_backward_long_runs():
+    """Embedding backward with long runs of one id (every token one of 9 ids, some outside the shard): the run
+    boundaries are found on the device (no host count of distinct ids), each id's row summed in token order."""
+    torch.manual_seed(1)
+    Vp, H = 8, 512
+    W = torch.randn(Vp, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    ids = torch.randint(0, 9, (6, 257), device=DEV) + 2  # ids 2..10; shard [4, 12) holds 4..10, ids 2 / 3 skipped
+    out = embedding.vocab_embedding(ids, W, 4, 12)
+    g = torch.randn_like(out)
+    out.backward(g)
+    flat, gi = g.reshape(-1, H).float(), ids.reshape(-1)
+    ref = torch.zeros(Vp, H, device=DEV)
+    for r in range(Vp):
+        sel = gi == r + 4
+        if sel.any():
+            ref[r] = flat[sel].sum(0)
+    torch.testing.assert_close(W.grad.float(), ref, atol=0.1, rtol=2e-2)
+
+
 def test_adamw_matches_torch():
     torch.manual_seed(0)
     n = 10007
