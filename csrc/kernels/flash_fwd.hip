@@ -196,6 +196,8 @@ struct FwdV2 {
 // profiles/attn_fwd_kt128_ab_r6.log (code in git history, commit "Drop the race-forensics build switches").
 // K / V staged through registers (buffer loads issued before a tile's MFMAs, ds_write after them, T14) instead of
 // LDS-DMA: 1.22-1.26 vs 1.13-1.16 ms, profiles/attn_fwd_regstage_ab_r6.log.
+// Half 1's exponentials scheduled into the gaps of half 0's P.V MFMAs (sched_group_barrier, bit-identical): 1.19-1.21
+// vs 1.17 ms, profiles/attn_fwd_pipe_ab_r6.log -- the loop is issue-bound at two waves per SIMD, not latency-bound.
 // NW = 4: 2 workgroups / CU = 2 waves / SIMD; NW = 6 (BM = 192): 2 workgroups / CU = 3 waves / SIMD (<= 168 VGPRs)
 #ifndef SA_FWD_NW
 #define SA_FWD_NW 4
