@@ -28,16 +28,24 @@ class CudaRNGStateTracker:
         gen.manual_seed(seed)
         self.state = gen.get_state()
 
+    def _generator(self) -> torch.Generator:
+        """The device's default generator, looked up once (``torch.cuda.get/set_rng_state`` re-resolve the device and
+        go through a lazy-call closure on every use: a fork per dropout costs that four times per call)."""
+        g = getattr(self, "_gen", None)
+        if g is None:
+            if self.device.type == "cuda":
+                idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+                g = torch.cuda.default_generators[idx]
+            else:
+                g = torch.default_generator
+            self._gen = g
+        return g
+
     def _get(self) -> torch.Tensor:
-        if self.device.type == "cuda":
-            return torch.cuda.get_rng_state(self.device)
-        return torch.get_rng_state()
+        return self._generator().get_state()
 
     def _set(self, state: torch.Tensor) -> None:
-        if self.device.type == "cuda":
-            torch.cuda.set_rng_state(state, self.device)
-        else:
-            torch.set_rng_state(state)
+        self._generator().set_state(state)
 
     def state_dict(self) -> RngTrackerState:
         return {"seed": self.seed, "state": self.state.clone().detach()}
