@@ -12,6 +12,7 @@
 #include "kernels/launch.h"
 
 void register_rehearsal(pybind11::module& m);  // rehearsal.cpp: asynchronous rehearsal worker
+void register_blaslt(pybind11::module& m);     // blaslt.cpp: small GEMMs through cached hipBLASLt plans
 
 namespace {
 
@@ -734,6 +735,7 @@ at::Tensor dropout_add(const at::Tensor& x_, const c10::optional<at::Tensor>& re
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "scaling_amd CDNA4 (gfx950) HIP kernels";
     register_rehearsal(m);
+    register_blaslt(m);
     m.def("norm_fwd", &norm_fwd, "RMSNorm/LayerNorm forward (optional fused residual add)", py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("layer"), py::arg("res") = py::none());
     m.def("norm_bwd", &norm_bwd, "RMSNorm/LayerNorm backward (optional fused residual-gradient add)", py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"), py::arg("layer"), py::arg("dadd") = py::none());
     m.def("swiglu_fwd", &swiglu_fwd, "SwiGLU forward");

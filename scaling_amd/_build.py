@@ -58,7 +58,7 @@ def _common_flags(inc: list[str]) -> list[str]:
 
 def _sources() -> list[Path]:
     """Sources of the torch/HIP extension ``_C`` (kernels + bindings)."""
-    return sorted(list((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp", CSRC / "rehearsal.cpp"])
+    return sorted(list((CSRC / "kernels").glob("*.hip")) + [CSRC / "bindings.cpp", CSRC / "rehearsal.cpp", CSRC / "blaslt.cpp"])
 
 
 def _data_sources() -> list[Path]:
@@ -184,7 +184,7 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out) + ".tmp"] + [str(o) for o in objs]
     for p in lib:
         cmd += [f"-L{p}", f"-Wl,-rpath,{p}"]
-    cmd += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lgomp"]
+    cmd += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lhipblaslt", "-lgomp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

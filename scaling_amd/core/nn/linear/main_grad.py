@@ -51,7 +51,7 @@ import torch.distributed as dist
 
 from ....ops.attention import stash_gemm
 from ....ops.gemm import linear as gemm_linear
-from ....ops.gemm import mm_nt, transpose2d, wgrad
+from ....ops.gemm import mm, mm_nt, transpose2d, wgrad
 from ...utils.debug_env import side_streams_enabled
 
 _GEN = [0]
@@ -253,7 +253,7 @@ class _MultiLinear(torch.autograd.Function):
             if ctx.has_wt:  # w is the cached W^T [K, N]: dX = g (W^T)^T in the forward GEMM layout
                 dx = mm_nt(g.reshape(-1, g.shape[-1]), w).view(*g.shape[:-1], w.shape[0])
             else:
-                dx = torch.matmul(g, w)
+                dx = mm(g, w)
             if ctx.tp_group is not None:  # TP input-gradient all-reduce overlapped with the wgrad GEMM below
                 dx = dx.contiguous()
                 work = dist.all_reduce(dx, group=ctx.tp_group, async_op=True)

@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ....ops.attention import stash_gemm
-from ....ops.gemm import mm_nt
+from ....ops.gemm import mm, mm_nt
 from ...utils.debug_env import side_streams_enabled
 from .main_grad import _adjacent, _MultiLinear, _rehome_adjacent, _transposed, weight_grads
 
@@ -252,7 +252,7 @@ class _SPGatherColumn(torch.autograd.Function):
         cs = _tp_comm_stream(g.device)
         main = torch.cuda.current_stream(g.device) if cs is not None else None
         if ctx.needs_input_grad[0]:
-            dx = mm_nt(g2, w) if ctx.has_wt else torch.matmul(g2, w)  # [T, K]
+            dx = mm_nt(g2, w) if ctx.has_wt else mm(g2, w)  # [T, K]
             shard = torch.empty((T // size, K), dtype=dx.dtype, device=dx.device)
             if cs is not None:
                 assert main is not None

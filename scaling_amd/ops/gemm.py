@@ -11,10 +11,11 @@ hipBLASLt runs this TN layout at 0.95-1.2 PF.  M / N need only be multiples of 1
 round 5).  Shapes it does not tile (M/N not multiples of 16, T not a multiple of 128) use ``torch.matmul`` /
 ``addmm_`` (hipBLASLt).
 
-``linear`` is the forward ``x W^T (+ b)`` of every linear layer and ``mm_nt`` the input gradient ``dY (W^T)^T`` on
-the cached transpose: at most 4 token rows (token-by-token decoding) run the weight-streaming GEMV kernel
-(``csrc/kernels/gemv.hip``); larger products are plain library GEMMs (hipBLASLt, TunableOp table
-``scaling_amd/tuning/gemm_gfx950.csv``).  A hand-written NT GEMM with fused SwiGLU epilogues (rounds 3-5) stayed
+``linear`` is the forward ``x W^T (+ b)`` of every linear layer, ``mm_nt`` the input gradient ``dY (W^T)^T`` on
+the cached transpose and ``mm`` the input gradient ``dY W`` without it: at most 4 token rows (token-by-token decoding)
+run the weight-streaming GEMV kernel (``csrc/kernels/gemv.hip``); small products (<= ``SCALING_AMD_LT_SMALL_FLOP``
+multiply-adds, 2^33 by default: none of the 7B step's) go through cached hipBLASLt plans (``csrc/blaslt.cpp``); the
+rest are plain library GEMMs (hipBLASLt through torch, TunableOp table ``scaling_amd/tuning/gemm_gfx950.csv``).  A hand-written NT GEMM with fused SwiGLU epilogues (rounds 3-5) stayed
 1-6 % behind hipBLASLt at every 7B shape and lost in the step even with its epilogues
 (``profiles/gemm_nt_round_remap_ab_r5.log``, ``profiles/swiglu_bwd_nt_ab_r5.log``); it was deleted in round 6.
 """
@@ -55,9 +56,34 @@ def transpose2d(x: torch.Tensor) -> torch.Tensor:
 
 
 GEMV_MAX_ROWS = 4
+# products of at most this many multiply-adds go through cached hipBLASLt plans (csrc/blaslt.cpp): torch's path
+# re-plans every call (~25-30 us of host time), which only a host-bound small model notices; 0 disables
+_LT_SMALL = int(os.environ.get("SCALING_AMD_LT_SMALL_FLOP", str(1 << 33)))
+
+
+def _lt_ok(a: torch.Tensor, w: torch.Tensor, m: int, n: int, k: int) -> bool:
+    # (torch's deterministic mode keeps its own library choice: the plans take hipBLASLt's first heuristic pick)
+    return (0 < m * n * k <= _LT_SMALL and a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)
+            and a.dtype == w.dtype and not torch.are_deterministic_algorithms_enabled())
+
+
+def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b`` for ``a`` [..., K] and 2-D ``b`` [K, N] (no autograd graph)."""
+    K, N = b.shape
+    a2 = a.reshape(-1, K)
+    if _lt_ok(a, b, a2.shape[0], N, K):
+        y = ext().lt_mm(a2.contiguous(), b.contiguous())
+        if y is not None:
+            return y.view(*a.shape[:-1], N)
+    return torch.matmul(a, b)
+
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``a @ b^T`` for 2-D ``a`` [M, K] and ``b`` [N, K] (no autograd graph; hipBLASLt)."""
+    """``a @ b^T`` for 2-D ``a`` [M, K] and ``b`` [N, K] (no autograd graph)."""
+    if _lt_ok(a, b, a.shape[0], b.shape[0], a.shape[1]):
+        y = ext().lt_linear(a.contiguous(), b.contiguous(), None)
+        if y is not None:
+            return y
     return torch.matmul(a, b.t())
 
 
@@ -73,4 +99,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
         x2 = x.reshape(rows, K)
         if ext().gemv_ok(x2, w) and (b is None or b.dtype == w.dtype):
             return ext().gemv(x2, w, b).reshape(*x.shape[:-1], w.shape[0])
+    if not needs_graph and w.dim() == 2 and _lt_ok(x, w, rows, w.shape[0], K) and (b is None or b.dtype == w.dtype):
+        y = ext().lt_linear(x.reshape(rows, K).contiguous(), w.contiguous(), b)
+        if y is not None:
+            return y.view(*x.shape[:-1], w.shape[0])
     return torch.nn.functional.linear(x, w, b)
