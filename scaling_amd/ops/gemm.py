@@ -64,7 +64,8 @@ _LT_SMALL = int(os.environ.get("SCALING_AMD_LT_SMALL_FLOP", str(1 << 33)))
 def _lt_ok(a: torch.Tensor, w: torch.Tensor, m: int, n: int, k: int) -> bool:
     # (torch's deterministic mode keeps its own library choice: the plans take hipBLASLt's first heuristic pick)
     return (0 < m * n * k <= _LT_SMALL and a.is_cuda and a.dtype in (torch.bfloat16, torch.float16)
-            and a.dtype == w.dtype and not torch.are_deterministic_algorithms_enabled())
+            and a.dtype == w.dtype and not torch.are_deterministic_algorithms_enabled()
+            and not torch.cuda.is_current_stream_capturing())  # (a plan made inside a capture would own graph memory)
 
 
 def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
