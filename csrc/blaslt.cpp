@@ -103,7 +103,10 @@ bool usable(const at::Tensor& t) {
 }
 
 // y = x2 @ w^T (+ b) for 2-D x2 [M, K], w [N, K]; an undefined tensor when no plan exists (the caller falls back)
-at::Tensor lt_linear(const at::Tensor& x2, const at::Tensor& w, const c10::optional<at::Tensor>& b) {
+// `out` (optional): a contiguous tensor of M * N elements to write (any shape: callers pass the un-flattened one, so
+// the result is not a view of a 2-D temporary)
+at::Tensor lt_linear(const at::Tensor& x2, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                     const c10::optional<at::Tensor>& out) {
     if (!usable(x2) || !usable(w) || x2.dim() != 2 || w.dim() != 2 || x2.size(1) != w.size(1) ||
         x2.scalar_type() != w.scalar_type())
         return at::Tensor();
@@ -115,13 +118,14 @@ at::Tensor lt_linear(const at::Tensor& x2, const at::Tensor& w, const c10::optio
     std::lock_guard<std::mutex> lk(state().m);
     Plan* p = plan_for(dev, M, N, K, 0, x2.scalar_type(), has_b);
     if (p == nullptr) return at::Tensor();
-    at::Tensor y = at::empty({M, N}, x2.options());
+    at::Tensor y = out.has_value() && out->defined() ? *out : at::empty({M, N}, x2.options());
+    TORCH_CHECK(y.is_contiguous() && y.numel() == M * N && y.scalar_type() == x2.scalar_type(), "lt_linear: out");
     if (!run(p, dev, w.data_ptr(), x2.data_ptr(), y.data_ptr(), has_b ? b->data_ptr() : nullptr)) return at::Tensor();
     return y;
 }
 
 // y = a @ bm for 2-D a [M, K], bm [K, N]
-at::Tensor lt_mm(const at::Tensor& a, const at::Tensor& bm) {
+at::Tensor lt_mm(const at::Tensor& a, const at::Tensor& bm, const c10::optional<at::Tensor>& out) {
     if (!usable(a) || !usable(bm) || a.dim() != 2 || bm.dim() != 2 || a.size(1) != bm.size(0) ||
         a.scalar_type() != bm.scalar_type())
         return at::Tensor();
@@ -131,7 +135,8 @@ at::Tensor lt_mm(const at::Tensor& a, const at::Tensor& bm) {
     std::lock_guard<std::mutex> lk(state().m);
     Plan* p = plan_for(dev, M, N, K, 1, a.scalar_type(), false);
     if (p == nullptr) return at::Tensor();
-    at::Tensor y = at::empty({M, N}, a.options());
+    at::Tensor y = out.has_value() && out->defined() ? *out : at::empty({M, N}, a.options());
+    TORCH_CHECK(y.is_contiguous() && y.numel() == M * N && y.scalar_type() == a.scalar_type(), "lt_mm: out");
     if (!run(p, dev, bm.data_ptr(), a.data_ptr(), y.data_ptr(), nullptr)) return at::Tensor();
     return y;
 }
@@ -140,6 +145,8 @@ at::Tensor lt_mm(const at::Tensor& a, const at::Tensor& bm) {
 
 void register_blaslt(pybind11::module& m) {
     m.def("lt_linear", &lt_linear, "small GEMM x @ w^T (+ b) through a cached hipBLASLt plan (undefined: no plan)",
-          pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b") = pybind11::none());
-    m.def("lt_mm", &lt_mm, "small GEMM a @ b through a cached hipBLASLt plan (undefined: no plan)");
+          pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b") = pybind11::none(),
+          pybind11::arg("out") = pybind11::none());
+    m.def("lt_mm", &lt_mm, "small GEMM a @ b through a cached hipBLASLt plan (undefined: no plan)", pybind11::arg("a"),
+          pybind11::arg("b"), pybind11::arg("out") = pybind11::none());
 }

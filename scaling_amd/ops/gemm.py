@@ -73,9 +73,9 @@ def mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     K, N = b.shape
     a2 = a.reshape(-1, K)
     if _lt_ok(a, b, a2.shape[0], N, K):
-        y = ext().lt_mm(a2.contiguous(), b.contiguous())
+        y = ext().lt_mm(a2.contiguous(), b.contiguous(), a.new_empty(*a.shape[:-1], N))
         if y is not None:
-            return y.view(*a.shape[:-1], N)
+            return y
     return torch.matmul(a, b)
 
 
@@ -101,7 +101,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
         if ext().gemv_ok(x2, w) and (b is None or b.dtype == w.dtype):
             return ext().gemv(x2, w, b).reshape(*x.shape[:-1], w.shape[0])
     if not needs_graph and w.dim() == 2 and _lt_ok(x, w, rows, w.shape[0], K) and (b is None or b.dtype == w.dtype):
-        y = ext().lt_linear(x.reshape(rows, K).contiguous(), w.contiguous(), b)
+        # (written into the un-flattened output: a view of a 2-D result would not be updatable in place -- the
+        # in-base LoRA up-projections accumulate into the q/k/v GEMM output)
+        y = ext().lt_linear(x.reshape(rows, K).contiguous(), w.contiguous(), b, x.new_empty(*x.shape[:-1], w.shape[0]))
         if y is not None:
-            return y.view(*x.shape[:-1], w.shape[0])
+            return y
     return torch.nn.functional.linear(x, w, b)
